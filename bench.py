@@ -1,0 +1,296 @@
+"""Benchmark of the coupling-flow hot path on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): 6-layer RealNVP affine
+coupling, D=10 logits, conditioner hidden_size=[5,5] (reference default,
+flows/flows.py:71), B=2^20 synthetic logit vectors per GPU, fp32.  One step =
+one fused forward + per-sample log-det pass over one batch (cnf_forward through
+the C ABI: final z [B,10] + log-det [B]).  With N>1 ranks every rank runs its
+own 2^20-vector shard (weak scaling, batch 8M at N=8 = configs[2]) and the step
+ends with the RCCL all-reduce of the shard's NLL sum (configs[2]).
+
+Inputs are resident in HBM before timing; the step rotates through enough
+distinct input/output buffers (>= --rotate-gb) that the 256 MB Infinity Cache
+cannot serve repeated launches.  Timing: HIP events on the launch stream
+around exactly --steps steps, barrier + synchronize on both sides, max over
+ranks.  Rank 0 prints one JSON line.
+"""
+import argparse
+import ctypes
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (ROOT, os.path.join(ROOT, "calibration-normalizing-flows_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
+VALU_PEAK_TFLOPS = 157.3  # FP32 vector peak (spec)
+MFMA_F32_PEAK_TFLOPS = 157.3
+
+WORKLOADS = {
+    # name: (D, L, hidden, B per GPU, inverse)
+    "cfg1": dict(D=3, L=2, hidden=[5, 5], B=4096, scale=False, inverse=False),
+    "cfg2": dict(D=10, L=6, hidden=[5, 5], B=1 << 20, scale=True, inverse=False),
+    "cfg4": dict(D=100, L=12, hidden=[100, 100], B=1 << 16, scale=True, inverse=False),
+    "cfg5": dict(D=10, L=6, hidden=[5, 5], B=1 << 20, scale=True, inverse=True),
+}
+
+
+def algo_flops_per_vec(D, L, hidden, scale=True):
+    """mask-reduced MACs, 2 flops each, + elementwise."""
+    dt, dc = D // 2, D - D // 2
+    units = [dc] + list(hidden) + [dt]
+    macs = sum(a * b for a, b in zip(units[:-1], units[1:]))
+    nets = 2 if scale else 1
+    per_layer = nets * 2 * macs + (3 * dt if scale else dt)
+    return L * per_layer
+
+
+def algo_bytes_per_vec(D, L, all_outputs=False):
+    return 4 * D + 4 * D * (L if all_outputs else 1) + 4
+
+
+def make_flow(w, device, seed=0):
+    from flows.flows import Flow, NvpCouplingLayer
+    torch.manual_seed(seed)
+    np.random.seed(seed)
+    flow = Flow([NvpCouplingLayer(w["D"], w["hidden"], scale=w["scale"]) for _ in range(w["L"])])
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for p in flow.parameters():
+            if p.requires_grad:  # N(0, 0.1): SURVEY 8(d) synthetic weights
+                p.copy_(torch.randn(p.shape, generator=g) * 0.1)
+    return flow.to(device)
+
+
+def synthetic_logits(B, D, device, seed):
+    """x = 2*onehot(y) + N(0,1), rows mean-centred (calibrators.py:17)."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    x = torch.randn(B, D, device=device, generator=g)
+    y = torch.randint(0, D, (B,), device=device, generator=g)
+    x[torch.arange(B, device=device), y] += 2.0
+    return x - x.mean(dim=1, keepdim=True), y
+
+
+class Runner:
+    """Pre-built C-ABI launches of one fused pass over rotating buffers."""
+
+    def __init__(self, w, device, rotate_bytes, all_outputs=False):
+        from cnf_hip import _lib
+        self.w = w
+        self.dev = device
+        self.flow = make_flow(w, device)
+        self.stack = self.flow._native_stack()
+        self.blob = self.stack.prepared(device)
+        self.lib = _lib.lib()
+        B, D, L = w["B"], w["D"], w["L"]
+        per_set = algo_bytes_per_vec(D, L, all_outputs) * B
+        self.nsets = max(1, min(64, math.ceil(rotate_bytes / per_set)))
+        self.sets = []
+        for i in range(self.nsets):
+            x, y = synthetic_logits(B, D, device, 1234 + i)
+            ld = torch.empty(B, device=device)
+            if all_outputs:
+                out, allt = None, torch.empty(L, B, D, device=device)
+            else:
+                out, allt = torch.empty(B, D, device=device), None
+            self.sets.append((x, y, out, ld, allt))
+        self.fn = self.lib.cnf_inverse if w["inverse"] else self.lib.cnf_forward
+        self.desc = ctypes.byref(self.stack.desc)
+        P = ctypes.c_void_p
+        vp = lambda t: P(t.data_ptr()) if t is not None else P(0)
+        self.stream = torch.cuda.current_stream(device)
+        self.args = [(vp(x), vp(out), vp(ld), vp(allt)) for (x, y, out, ld, allt) in self.sets]
+        self.i = 0
+
+    def step(self):
+        a = self.args[self.i % self.nsets]
+        self.i += 1
+        st = self.fn(self.desc, ctypes.c_void_p(self.blob.data_ptr()), a[0], a[1], a[2], a[3],
+                     ctypes.c_int64(self.w["B"]), ctypes.c_void_p(self.stream.cuda_stream))
+        if st != 0:
+            raise RuntimeError("cnf launch failed: %d" % st)
+
+    def timed(self, steps, warmup, collective=None):
+        for _ in range(warmup):
+            self.step()
+            if collective:
+                collective()
+        torch.cuda.synchronize(self.dev)
+        if dist.is_initialized():
+            dist.barrier()
+        torch.cuda.synchronize(self.dev)
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(self.stream)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            self.step()
+            if collective:
+                collective()
+        e1.record(self.stream)
+        torch.cuda.synchronize(self.dev)
+        wall = time.perf_counter() - t0
+        if dist.is_initialized():
+            dist.barrier()
+        torch.cuda.synchronize(self.dev)
+        return e0.elapsed_time(e1) / 1e3, wall
+
+
+def kernel_only_seconds(runner, launches):
+    """Average device time per launch over `launches` back-to-back launches
+    (HIP events on the launch stream, no collective in between)."""
+    t, _ = runner.timed(launches, 3)
+    return t / launches
+
+
+def cpu_baseline(w, seconds=10.0):
+    """The op-for-op torch CPU port (oracle/cnf_torch_port.py) on host cores."""
+    from oracle import cnf_torch_port as P
+    flow = make_flow(w, "cpu")
+    st = {k: v for k, v in flow.state_dict().items()}
+    layers = P.layers_from_state(st, w["L"], len(w["hidden"]) + 1, w["scale"], True)
+    B = min(w["B"], 1 << 18)
+    x, _ = synthetic_logits(B, w["D"], "cpu", 99)
+    P.flow_forward(layers, x)
+    times = []
+    t_start = time.perf_counter()
+    while time.perf_counter() - t_start < seconds or len(times) < 3:
+        t = time.perf_counter()
+        P.flow_forward(layers, x)
+        times.append(time.perf_counter() - t)
+    rate = B / float(np.median(times))
+    return {"value": rate, "unit": "logit-vectors/sec", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": "%d x %d-vector forward passes (B=%d, D=%d, L=%d, h=%s) with the "
+                      "op-for-op torch CPU port, median; port/reference cost ratio 1.00 "
+                      "on 8 cores (DESIGN.md)" % (len(times), B, B, w["D"], w["L"], w["hidden"])}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
+    ap.add_argument("--batch", type=int, default=0, help="vectors per GPU (default: config)")
+    ap.add_argument("--rotate-gb", type=float, default=1.0)
+    ap.add_argument("--no-variants", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    w = dict(WORKLOADS[args.workload])
+    if args.batch:
+        w["B"] = args.batch
+    runner = Runner(w, dev, args.rotate_gb * 1e9)
+
+    collective = None
+    if world > 1:
+        # NLL all-reduce over xGMI (configs[2]): each rank reduces its shard's
+        # per-row log-det sum; one 2-float RCCL all-reduce per step.
+        red = torch.zeros(2, device=dev)
+
+        def collective():
+            ld = runner.sets[(runner.i - 1) % runner.nsets][3]
+            red[0] = ld.sum()
+            red[1] = float(w["B"])
+            dist.all_reduce(red)
+        collective = collective
+
+    t_dev, wall = runner.timed(args.steps, args.warmup, collective)
+    t = torch.tensor([t_dev], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    t_max = t.item()
+    total_vecs = w["B"] * world * args.steps
+    value = total_vecs / t_max
+
+    # dominant kernel: average device time per launch, no collective in between
+    k_avg = kernel_only_seconds(runner, max(50, args.steps // 2))
+    bytes_vec = algo_bytes_per_vec(w["D"], w["L"])
+    flops_vec = algo_flops_per_vec(w["D"], w["L"], w["hidden"], w["scale"])
+    achieved_gbs = w["B"] * bytes_vec / k_avg / 1e9
+    achieved_tf = w["B"] * flops_vec / k_avg / 1e12
+    mfma_bound = w["D"] >= 32
+    roof = {
+        "bound": "mfma" if mfma_bound else "hbm",
+        "achieved": round(achieved_tf if mfma_bound else achieved_gbs, 2),
+        "peak": MFMA_F32_PEAK_TFLOPS if mfma_bound else HBM_PEAK_GBS,
+        "unit": "TFLOP/s" if mfma_bound else "GB/s",
+        "frac": None, "traffic": None,
+        "kernel": runner.stack.kernel_name(),
+        "kernel_avg_us": round(k_avg * 1e6, 3),
+        "algo_bytes_per_vec": bytes_vec, "algo_flops_per_vec": flops_vec,
+        "valu_tflops": round(achieved_tf, 2), "valu_frac": round(achieved_tf / VALU_PEAK_TFLOPS, 4),
+        "rotating_sets": runner.nsets,
+    }
+    roof["frac"] = round(roof["achieved"] / roof["peak"], 4)
+
+    variants = {}
+    if rank == 0 and world == 1 and not args.no_variants:
+        for name, wl, allo in (("cfg2_all_zs", WORKLOADS["cfg2"], True),
+                               ("cfg5_inverse", WORKLOADS["cfg5"], False),
+                               ("cfg4_d100", WORKLOADS["cfg4"], False)):
+            r = Runner(dict(wl), dev, args.rotate_gb * 1e9, all_outputs=allo)
+            ka = kernel_only_seconds(r, 30)
+            bv = algo_bytes_per_vec(wl["D"], wl["L"], allo)
+            fv = algo_flops_per_vec(wl["D"], wl["L"], wl["hidden"], wl["scale"])
+            variants[name] = {"vec_per_s": round(wl["B"] / ka, 1), "kernel_avg_us": round(ka * 1e6, 2),
+                              "B": wl["B"], "kernel": r.stack.kernel_name(),
+                              "hbm_gbs": round(wl["B"] * bv / ka / 1e9, 1),
+                              "tflops": round(wl["B"] * fv / ka / 1e12, 2)}
+            del r
+            torch.cuda.empty_cache()
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(w, args.cpu_seconds)
+
+    if rank == 0:
+        out = {
+            "metric": "logit-vectors/sec forward+log-det (6-layer RealNVP, D=10)"
+                      if args.workload == "cfg2" else "logit-vectors/sec (%s)" % args.workload,
+            "value": round(value, 1),
+            "unit": "logit-vectors/sec",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(t_max / args.steps * 1e3, 5),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f32", "data": "synthetic",
+            "config": {"workload": "%s: %d-layer %s coupling, D=%d, hidden_size=%s, %d vectors "
+                                   "per GPU%s" % (args.workload, w["L"],
+                                                  "RealNVP" if w["scale"] else "NICE", w["D"],
+                                                  w["hidden"], w["B"],
+                                                  ", inverse" if w["inverse"] else ""),
+                       "global_batch": w["B"] * world, "parallelism": "dp%d" % world,
+                       "hidden_size": w["hidden"], "weights": "N(0,0.1) synthetic"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "wall_s": round(wall, 4),
+        }
+        if variants:
+            out["variants"] = variants
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

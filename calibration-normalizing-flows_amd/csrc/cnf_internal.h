@@ -1,0 +1,72 @@
+// Internal declarations shared by the libcnf_hip translation units.
+// Shapes are derived once from cnf_desc (include/cnf.h); every kernel family
+// reads the same "prepared" blob prefix (index tables) followed by its own
+// weight layout.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "cnf.h"
+
+namespace cnf {
+
+constexpr int kMaxLin = CNF_MAX_HIDDEN + 1;  // Linear layers per conditioner MLP
+
+// Per-layer flags stored in the prepared blob.
+constexpr int32_t kFlagPerm = 1;  // layer has a random_flip permutation
+
+enum class Family { kValu, kTile };
+
+// Host-side view of a descriptor.
+struct Shape {
+  int D = 0, DT = 0, DC = 0, L = 0;  // DT: transformed (mask 0), DC: conditioning (mask 1)
+  int n_lin = 0;                     // Linear layers per net
+  int units[kMaxLin + 1] = {};       // [D, h..., D]
+  int scale = 1, shift = 1, strict = 0;
+  int nets = 2;                      // scale + shift
+  int64_t net_floats = 0;            // natural layout (state_dict order)
+  int64_t layer_floats = 0;
+  bool any_perm = false;
+  const int64_t* perms_host = nullptr;  // desc->perms (valid during the call)
+  Family family = Family::kTile;
+  int valu_id = -1;                  // index into the VALU instantiation table
+  // tile (MFMA) layout
+  int NO = 0;                        // last-linear outputs computed: DT (fast) or D (strict)
+  int lin_nin[kMaxLin] = {}, lin_nout[kMaxLin] = {}, lin_inoff[kMaxLin] = {};
+  int lin_OT[kMaxLin] = {}, lin_KS[kMaxLin] = {};
+  int64_t tile_lin_off[kMaxLin] = {};  // float offset of linear i within a tiled net
+  int64_t tile_net_floats = 0, tile_layer_floats = 0;
+  int tile_hp = 0;                   // padded activation rows
+  int tile_nop = 0;                  // padded S/T rows
+  int tile_waves = 0;                // waves per block that fit LDS
+  size_t tile_lds_bytes = 0;
+};
+
+// Prepared blob: [int32 fwd_q L*D][int32 inv_q L*D][int32 flags L] padded to
+// 256 B, then the weights region.
+inline int64_t idx_bytes(const Shape& s) {
+  int64_t b = (int64_t)(2 * s.L * s.D + s.L) * 4;
+  return (b + 255) / 256 * 256;
+}
+
+int derive_shape(const cnf_desc* d, Shape* s);
+void set_hip_error(hipError_t e);
+
+// ---- kernel-family entry points (return cnf_status) ----
+int valu_supported(const Shape& s);  // -> valu_id or -1
+int valu_run(const Shape& s, const void* prepared, const float* in, float* out, float* ld,
+             float* all, int64_t B, bool inverse, hipStream_t st);
+
+int tile_configure(Shape* s);        // fills tile_* fields; CNF_OK or UNSUPPORTED
+int tile_run(const Shape& s, const void* prepared, const float* in, float* out, float* ld,
+             float* all, int64_t B, bool inverse, hipStream_t st);
+
+int prepare_run(const Shape& s, const float* const* params, void* prepared, hipStream_t st);
+
+int vjp_workspace(const Shape& s, int64_t B, size_t* bytes);
+int vjp_run(const Shape& s, const void* prepared, const float* x, const int64_t* y, int kind,
+            float det, float grad_scale, float* loss_terms, float* grads, float* dx, int64_t B,
+            void* ws, size_t ws_bytes, hipStream_t st);
+
+}  // namespace cnf

@@ -1,0 +1,390 @@
+// General-shape coupling kernel on the f32 matrix cores (MFMA).
+//
+// Serves every NvpCouplingLayer stack the narrow VALU kernel does not: wide
+// logit vectors (CIFAR-100: D=100, hidden_size=[100,100]), any number of
+// hidden layers, any widths up to CNF_MAX_WIDTH.  One wave owns 16 logit
+// vectors for the whole L-layer stack; its activations live in LDS laid out
+// feature-major ([feature][16 vectors]), which is exactly the B-operand layout
+// of v_mfma_f32_16x16x4_f32 (lane l reads B[k = l>>4][j = l&15]), so each
+// Linear is a chain of MFMAs whose A operand is a pre-tiled, coalesced 256-B
+// slice of the weights (one per lane per MFMA, prepared by cnf_prepare).
+// f32-in/f32-acc MFMA is an exact fmaf chain -- no reduced precision.
+//
+// Per layer (flows/flows.py:101-126): s-net and t-net on the conditioning half
+// (mask-reduced K), fused bias + ReLU epilogues (flows/utils.py:26-31), the
+// affine update and the log-det partial sums in registers, then the flip /
+// random permutation as an LDS gather through the layer's index table.
+#include <hip/hip_runtime.h>
+
+#include "cnf_internal.h"
+
+namespace cnf {
+namespace {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+constexpr int kWaves = 4;  // max waves (16-vector tiles) per block
+constexpr int kTileRows = 16;
+
+struct TileArgs {
+  int D, DT, DC, NO, L, n_lin, scale, shift;
+  int nout[kMaxLin], OT[kMaxLin], KS[kMaxLin];
+  int64_t lin_off[kMaxLin];  // float offset of linear i inside a tiled net
+  int64_t net_floats, layer_floats;
+  int Dp, Hp, NOp;           // LDS rows of X, activation and S/T buffers
+  int wave_floats;           // LDS floats per wave
+};
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <bool STRICT>
+__device__ __forceinline__ float relu(float a) {
+  if constexpr (STRICT) return a < 0.f ? 0.f : a;
+  else return fmaxf(a, 0.f);
+}
+
+template <bool STRICT>
+__device__ __forceinline__ void epilogue(const floatx4& acc, int ot, const float* __restrict__ bias,
+                                         float* OUT, int nout, bool do_relu, float p0, int lane) {
+  const int c = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int o = ot * 16 + 4 * g + r;
+    float v = acc[r] + bias[o] + p0;
+    if (do_relu) v = relu<STRICT>(v);
+    OUT[o * kTileRows + c] = o < nout ? v : 0.f;
+  }
+}
+
+// OUT[o][j] = act(bias[o] + sum_k W[o][k] * IN[k][j]) for o < OT*16, j < 16.
+template <bool STRICT>
+__device__ __forceinline__ void gemm(const float* __restrict__ lin, const float* IN, float* OUT,
+                                     int OT, int KS, int nout, bool do_relu, float p0, int lane) {
+  const float* __restrict__ bias = lin;
+  const float* __restrict__ tiles = lin + OT * 16;
+  const int boff = (lane >> 4) * kTileRows + (lane & 15);
+  for (int ot = 0; ot < OT; ot += 2) {
+    const bool two = ot + 1 < OT;
+    floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    const float* __restrict__ w0 = tiles + (int64_t)ot * KS * 64 + lane;
+    const float* __restrict__ w1 = w0 + KS * 64;
+    if (two) {
+#pragma unroll 4
+      for (int ks = 0; ks < KS; ++ks) {
+        const float b = IN[ks * 4 * kTileRows + boff];
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(w0[ks * 64], b, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(w1[ks * 64], b, acc1, 0, 0, 0);
+      }
+    } else {
+      for (int ks = 0; ks < KS; ++ks) {
+        const float b = IN[ks * 4 * kTileRows + boff];
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(w0[ks * 64], b, acc0, 0, 0, 0);
+      }
+    }
+    epilogue<STRICT>(acc0, ot, bias, OUT, nout, do_relu, p0, lane);
+    if (two) epilogue<STRICT>(acc1, ot + 1, bias, OUT, nout, do_relu, p0, lane);
+  }
+}
+
+// One conditioner MLP: conditioning rows of X -> OUT rows [0, NO).
+template <bool STRICT>
+__device__ __forceinline__ void mlp(const TileArgs& a, const float* __restrict__ net,
+                                    const float* Xc, float* A0, float* A1, float* OUT, float p0,
+                                    int lane) {
+  const float* in = Xc;
+  for (int i = 0; i < a.n_lin; ++i) {
+    const bool last = i == a.n_lin - 1;
+    float* o = last ? OUT : ((i & 1) ? A1 : A0);
+    gemm<STRICT>(net + a.lin_off[i], in, o, a.OT[i], a.KS[i], a.nout[i], !last,
+                 i == 0 ? p0 : 0.f, lane);
+    wave_sync();
+    in = o;
+  }
+}
+
+template <bool INV, bool STRICT>
+__global__ __launch_bounds__(256) void k_tile(TileArgs a, const float* __restrict__ W,
+                                              const int32_t* __restrict__ qtab,
+                                              const float* __restrict__ in,
+                                              float* __restrict__ out, float* __restrict__ ld_out,
+                                              float* __restrict__ all, int64_t B) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nw = blockDim.x >> 6;
+  const int64_t row0 = ((int64_t)blockIdx.x * nw + wave) * kTileRows;
+  if (row0 >= B) return;  // only wave-local synchronisation below
+  const int nrows = (int)((B - row0) < kTileRows ? (B - row0) : kTileRows);
+  const int D = a.D, DT = a.DT;
+  float* X = smem + (int64_t)wave * a.wave_floats;
+  float* Xn = X + a.Dp * kTileRows;
+  float* A0 = Xn + a.Dp * kTileRows;
+  float* A1 = A0 + a.Hp * kTileRows;
+  float* S = A1 + a.Hp * kTileRows;
+  float* T = S + a.NOp * kTileRows;
+  const int c = lane & 15;
+
+  for (int i = D * kTileRows + lane; i < a.Dp * kTileRows; i += 64) X[i] = Xn[i] = 0.f;
+  const float* src = in + row0 * D;
+  for (int i = lane; i < kTileRows * D; i += 64) {
+    const int r = i / D, f = i - r * D;
+    X[f * kTileRows + r] = r < nrows ? src[i] : 0.f;
+  }
+  wave_sync();
+
+  float ld = 0.f;
+  for (int st = 0; st < a.L; ++st) {
+    const int l = INV ? a.L - 1 - st : st;
+    const int32_t* __restrict__ q = qtab + l * D;
+    if constexpr (INV) {  // z.flip(1) then z[:, rev_perm]  (flows/flows.py:115-117)
+      for (int i = lane; i < D * kTileRows; i += 64) {
+        const int j = i >> 4;
+        Xn[i] = X[q[j] * kTileRows + (i & 15)];
+      }
+      wave_sync();
+      float* t = X; X = Xn; Xn = t;
+    }
+    float p0 = 0.f;
+    if constexpr (STRICT) {
+      for (int j = 0; j < DT; ++j) p0 += 0.f * X[j * kTileRows + c];
+    }
+    const float* __restrict__ wl = W + (int64_t)l * a.layer_floats;
+    if (a.scale) {
+      mlp<STRICT>(a, wl, X + DT * kTileRows, A0, A1, S, p0, lane);
+      wl += a.net_floats;
+    }
+    if (a.shift) mlp<STRICT>(a, wl, X + DT * kTileRows, A0, A1, T, p0, lane);
+    const int nupd = STRICT ? D : DT;
+    for (int i = lane; i < nupd * kTileRows; i += 64) {
+      const int j = i >> 4;
+      const float x = X[i];
+      const float s = a.scale ? S[i] : 0.f;
+      const float t = a.shift ? T[i] : 0.f;
+      float y = INV ? (x - t) * expf(-s) : fmaf(x, expf(s), t);
+      if (j < DT) {
+        X[i] = STRICT ? 0.f * x + y : y;
+        ld += INV ? -s : s;
+      } else {  // STRICT only: masked position keeps x unless exp overflowed
+        X[i] = x + 0.f * y;
+        ld += 0.f * s;
+      }
+    }
+    wave_sync();
+    if constexpr (!INV) {  // z[:, perm] then z.flip(1)  (flows/flows.py:110-112)
+      for (int i = lane; i < D * kTileRows; i += 64) {
+        const int j = i >> 4;
+        Xn[i] = X[q[j] * kTileRows + (i & 15)];
+      }
+      wave_sync();
+      float* t = X; X = Xn; Xn = t;
+    }
+    if (all) {
+      float* dst = all + (int64_t)st * B * D + row0 * D;
+      for (int i = lane; i < nrows * D; i += 64) {
+        const int r = i / D, f = i - r * D;
+        dst[i] = X[f * kTileRows + r];
+      }
+    }
+  }
+  if (out) {
+    float* dst = out + row0 * D;
+    for (int i = lane; i < nrows * D; i += 64) {
+      const int r = i / D, f = i - r * D;
+      dst[i] = X[f * kTileRows + r];
+    }
+  }
+  ld += __shfl_xor(ld, 16);
+  ld += __shfl_xor(ld, 32);
+  if (ld_out && lane < nrows) ld_out[row0 + lane] = ld;
+}
+
+TileArgs make_args(const Shape& s) {
+  TileArgs a{};
+  a.D = s.D; a.DT = s.DT; a.DC = s.DC; a.NO = s.NO; a.L = s.L; a.n_lin = s.n_lin;
+  a.scale = s.scale; a.shift = s.shift;
+  for (int i = 0; i < s.n_lin; ++i) {
+    a.nout[i] = s.lin_nout[i];
+    a.OT[i] = s.lin_OT[i];
+    a.KS[i] = s.lin_KS[i];
+    a.lin_off[i] = s.tile_lin_off[i];
+  }
+  a.net_floats = s.tile_net_floats;
+  a.layer_floats = s.tile_layer_floats;
+  a.Dp = (s.D + 3) / 4 * 4 + 4;
+  a.Hp = s.tile_hp;
+  a.NOp = s.tile_nop;
+  a.wave_floats = (2 * a.Dp + 2 * a.Hp + 2 * a.NOp) * kTileRows;
+  return a;
+}
+
+// ---------------------------------------------------------------------------
+// cnf_prepare: one launch per layer; the parameter pointers and the layer's
+// index tables travel by value in the kernel arguments (no host staging).
+// ---------------------------------------------------------------------------
+struct PrepSeg {
+  const float* W;
+  const float* b;
+  int64_t dst;  // float offset in the weights region
+  int mode;     // 0: natural copy (W then b), 1: MFMA tiles
+  int nout_full, nin_full, in_off, nin, nout, OT, KS;
+};
+
+struct PrepArgs {
+  PrepSeg seg[2 * kMaxLin];
+  int nseg, layer, D, L;
+  int32_t flag;
+  int32_t fq[CNF_MAX_DIM], iq[CNF_MAX_DIM];
+};
+
+__global__ void k_prepare(PrepArgs a, float* __restrict__ wreg, int32_t* __restrict__ idx) {
+  if ((int)blockIdx.x == a.nseg) {
+    for (int j = threadIdx.x; j < a.D; j += blockDim.x) {
+      idx[a.layer * a.D + j] = a.fq[j];
+      idx[a.L * a.D + a.layer * a.D + j] = a.iq[j];
+    }
+    if (threadIdx.x == 0) idx[2 * a.L * a.D + a.layer] = a.flag;
+    return;
+  }
+  const PrepSeg& g = a.seg[blockIdx.x];
+  float* dst = wreg + g.dst;
+  if (g.mode == 0) {
+    const int64_t nW = (int64_t)g.nout_full * g.nin_full;
+    for (int64_t i = threadIdx.x; i < nW + g.nout_full; i += blockDim.x)
+      dst[i] = i < nW ? g.W[i] : g.b[i - nW];
+    return;
+  }
+  for (int o = threadIdx.x; o < g.OT * 16; o += blockDim.x) dst[o] = o < g.nout ? g.b[o] : 0.f;
+  const int64_t ntile = (int64_t)g.OT * g.KS * 64;
+  float* tiles = dst + g.OT * 16;
+  for (int64_t e = threadIdx.x; e < ntile; e += blockDim.x) {
+    const int64_t ot = e / (g.KS * 64);
+    const int rem = (int)(e - ot * g.KS * 64);
+    const int ks = rem >> 6, ln = rem & 63;
+    const int o = (int)ot * 16 + (ln & 15), k = ks * 4 + (ln >> 4);
+    tiles[e] = (o < g.nout && k < g.nin) ? g.W[(int64_t)o * g.nin_full + g.in_off + k] : 0.f;
+  }
+}
+
+}  // namespace
+
+int tile_configure(Shape* s) {
+  s->NO = s->strict ? s->D : s->DT;
+  int hp = 16;
+  int64_t off = 0;
+  for (int i = 0; i < s->n_lin; ++i) {
+    const int nin_full = s->units[i], nout_full = s->units[i + 1];
+    const bool first = i == 0, last = i == s->n_lin - 1;
+    const int nin = first ? s->DC : nin_full;
+    const int nout = last ? s->NO : nout_full;
+    s->lin_nin[i] = nin;
+    s->lin_nout[i] = nout;
+    s->lin_inoff[i] = first ? s->DT : 0;
+    s->lin_OT[i] = (nout + 15) / 16;
+    s->lin_KS[i] = (nin + 3) / 4;
+    s->tile_lin_off[i] = off;
+    off += (int64_t)s->lin_OT[i] * 16 + (int64_t)s->lin_OT[i] * s->lin_KS[i] * 64;
+    if (!last && s->lin_OT[i] * 16 > hp) hp = s->lin_OT[i] * 16;
+    if (nout_full > CNF_MAX_WIDTH || nin_full > CNF_MAX_WIDTH) return CNF_ERR_UNSUPPORTED;
+  }
+  s->tile_net_floats = off;
+  s->tile_layer_floats = off * s->nets;
+  s->tile_hp = hp;
+  s->tile_nop = (s->NO + 15) / 16 * 16;
+  const int dp = (s->D + 3) / 4 * 4 + 4;
+  const size_t per_wave = (size_t)(2 * dp + 2 * hp + 2 * s->tile_nop) * kTileRows * 4;
+  int waves = (int)((160 * 1024) / per_wave);
+  if (waves < 1) return CNF_ERR_UNSUPPORTED;
+  if (waves > kWaves) waves = kWaves;
+  s->tile_waves = waves;
+  s->tile_lds_bytes = per_wave * waves;
+  return CNF_OK;
+}
+
+int tile_run(const Shape& s, const void* prepared, const float* in, float* out, float* ld,
+             float* all, int64_t B, bool inverse, hipStream_t st) {
+  if (B == 0) return CNF_OK;
+  TileArgs a = make_args(s);
+  const char* base = static_cast<const char*>(prepared);
+  const int32_t* fwd_q = reinterpret_cast<const int32_t*>(base);
+  const int32_t* inv_q = fwd_q + s.L * s.D;
+  const float* W = reinterpret_cast<const float*>(base + idx_bytes(s));
+  const int64_t vecs_per_block = (int64_t)s.tile_waves * kTileRows;
+  dim3 grid((unsigned)((B + vecs_per_block - 1) / vecs_per_block)), block(64 * s.tile_waves);
+  auto fn = inverse ? (s.strict ? k_tile<true, true> : k_tile<true, false>)
+                    : (s.strict ? k_tile<false, true> : k_tile<false, false>);
+  hipLaunchKernelGGL(fn, grid, block, s.tile_lds_bytes, st, a, W, inverse ? inv_q : fwd_q, in, out,
+                     ld, all, B);
+  hipError_t err = hipGetLastError();
+  if (err != hipSuccess) {
+    set_hip_error(err);
+    return CNF_ERR_HIP;
+  }
+  return CNF_OK;
+}
+
+int prepare_run(const Shape& s, const float* const* params, void* prepared, hipStream_t st) {
+  char* base = static_cast<char*>(prepared);
+  int32_t* idx = reinterpret_cast<int32_t*>(base);
+  float* wreg = reinterpret_cast<float*>(base + idx_bytes(s));
+  const bool tiled = s.family == Family::kTile;
+  int pi = 0;
+  for (int l = 0; l < s.L; ++l) {
+    PrepArgs a{};
+    a.layer = l;
+    a.D = s.D;
+    a.L = s.L;
+    a.nseg = 0;
+    int64_t dst = tiled ? (int64_t)l * s.tile_layer_floats : (int64_t)l * s.layer_floats;
+    for (int net = 0; net < s.nets; ++net) {
+      for (int i = 0; i < s.n_lin; ++i) {
+        PrepSeg& g = a.seg[a.nseg++];
+        g.W = params[pi++];
+        g.b = params[pi++];
+        if (!g.W || !g.b) return CNF_ERR_NULL;
+        g.nout_full = s.units[i + 1];
+        g.nin_full = s.units[i];
+        if (tiled) {
+          g.mode = 1;
+          g.in_off = s.lin_inoff[i];
+          g.nin = s.lin_nin[i];
+          g.nout = s.lin_nout[i];
+          g.OT = s.lin_OT[i];
+          g.KS = s.lin_KS[i];
+          g.dst = dst + s.tile_lin_off[i];
+        } else {
+          g.mode = 0;
+          g.dst = dst;
+          dst += (int64_t)g.nout_full * g.nin_full + g.nout_full;
+        }
+      }
+      if (tiled) dst += s.tile_net_floats;
+    }
+    const int64_t* perm = nullptr;
+    if (s.any_perm && s.perms_host) {
+      const int64_t* p = s.perms_host + (int64_t)l * s.D;
+      if (p[0] >= 0) perm = p;
+    }
+    a.flag = perm ? kFlagPerm : 0;
+    int32_t rev[CNF_MAX_DIM];
+    if (perm) {
+      for (int j = 0; j < s.D; ++j) rev[perm[j]] = j;
+    }
+    for (int j = 0; j < s.D; ++j) {
+      // forward: out[j] = z[perm[D-1-j]]; inverse: x_in[j] = z[D-1-rev_perm[j]]
+      a.fq[j] = perm ? (int32_t)perm[s.D - 1 - j] : s.D - 1 - j;
+      a.iq[j] = perm ? s.D - 1 - rev[j] : s.D - 1 - j;
+    }
+    hipLaunchKernelGGL(k_prepare, dim3(a.nseg + 1), dim3(256), 0, st, a, wreg, idx);
+    hipError_t err = hipGetLastError();
+    if (err != hipSuccess) {
+      set_hip_error(err);
+      return CNF_ERR_HIP;
+    }
+  }
+  return CNF_OK;
+}
+
+}  // namespace cnf

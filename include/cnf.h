@@ -1,0 +1,133 @@
+/*
+ * cnf.h -- C ABI of libcnf_hip.so, the MI355X (gfx950) coupling-flow engine.
+ *
+ * Drop-in native boundary for the RealNVP / NICE forward, inverse and
+ * log|det J| path of the reference (SergioAlvarezB/calibration-normalizing-flows):
+ *
+ *   cnf_forward   replaces Flow.forward            flows/flows.py:17-25
+ *                 (NvpCouplingLayer.forward         flows/flows.py:101-112,
+ *                  MLP.forward                      flows/utils.py:26-31)
+ *   cnf_inverse   replaces Flow.backward           flows/flows.py:27-37
+ *                 (NvpCouplingLayer.backward        flows/flows.py:114-126 -- the
+ *                  reference's "backward" is the INVERSE transform, not autograd)
+ *   cnf_prepare   replaces the per-layer parameter reads of the above
+ *                 (state_dict layout: flows/flows.py:76-99, flows/utils.py:14-22)
+ *   cnf_loss_vjp  replaces autograd of the calibrator loss
+ *                 calibrators.py:287-295 / run_experiment3D.py:102-107
+ *
+ * Plain C: pointers + sizes, no torch types.  Every device pointer is a HIP
+ * device allocation owned by the caller; all work is enqueued on the caller's
+ * stream (hipStream_t passed as void*), nothing synchronises the host, nothing
+ * allocates, so every entry point is graph-capturable (cnf_prepare included
+ * once its host tables are built -- see below).  Errors are returned as
+ * negative cnf_status codes; no exception crosses the ABI.
+ *
+ * Data layout: row-major fp32 logit batches [B][D] (one logit vector per row).
+ */
+#ifndef CNF_H_
+#define CNF_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CNF_ABI_VERSION 1
+#define CNF_MAX_HIDDEN 8    /* hidden layers per conditioner MLP            */
+#define CNF_MAX_DIM 256     /* logit-vector width D                         */
+#define CNF_MAX_WIDTH 512   /* any MLP width                                */
+
+typedef enum cnf_status {
+  CNF_OK = 0,
+  CNF_ERR_NULL = -1,          /* a required pointer is NULL                   */
+  CNF_ERR_DESC = -2,          /* malformed descriptor (dims, abi_version)     */
+  CNF_ERR_UNSUPPORTED = -3,   /* shape outside every kernel's envelope        */
+  CNF_ERR_BATCH = -4,         /* negative batch                               */
+  CNF_ERR_HIP = -5,           /* a HIP launch/copy failed (cnf_last_hip_error) */
+  CNF_ERR_ALIGN = -6          /* pointer not 4-byte aligned                   */
+} cnf_status;
+
+/* The shape of one Flow made of NvpCouplingLayers (flows/flows.py:68-99). */
+typedef struct cnf_desc {
+  int32_t abi_version;          /* = CNF_ABI_VERSION                              */
+  int32_t dim;                  /* D (n_classes), 2..CNF_MAX_DIM                  */
+  int32_t n_layers;             /* L >= 1                                         */
+  int32_t n_hidden;             /* len(hidden_size), 0..CNF_MAX_HIDDEN            */
+  int32_t hidden[CNF_MAX_HIDDEN];
+  int32_t scale;                /* 1: s-net present (RealNVP); 0: NICE, s == 0    */
+  int32_t shift;                /* 1: t-net present; 0: t == 0                    */
+  int32_t strict_nan;           /* 1: reproduce the reference's inf*0 = NaN at
+                                   masked positions (flows/flows.py:107,123)      */
+  int32_t reserved;
+  const int64_t* perms;         /* HOST pointer, NULL or L*D entries: layer l's
+                                   random_flip permutation (flows/flows.py:92-99);
+                                   a row whose first entry is < 0 = no perm      */
+} cnf_desc;
+
+/* One float per parameter, in the reference's state_dict order. */
+int cnf_param_count(const cnf_desc* desc, int64_t* n_floats);
+
+/* Number of parameter tensors cnf_prepare expects, in this order per layer
+ * l = 0..L-1:  [s.layers.0.weight, s.layers.0.bias, ..., s.layers.k.bias]
+ * (if scale), then the same for t (if shift).  Weight [out][in] row-major. */
+int cnf_param_tensor_count(const cnf_desc* desc, int32_t* n_tensors);
+
+/* Bytes of the device blob cnf_prepare writes (kernel-specific layout). */
+int cnf_prepared_bytes(const cnf_desc* desc, size_t* bytes);
+
+/* Reformat the parameters into the blob the selected kernel reads: the mask,
+ * the per-layer flip and any random_flip permutation are folded into index
+ * tables; weights are restricted to the unmasked block and tiled for the
+ * kernel.  params: HOST array of cnf_param_tensor_count DEVICE pointers. */
+int cnf_prepare(const cnf_desc* desc, const float* const* params, void* prepared,
+                void* stream);
+
+/* Forward + per-sample log-det (Flow.forward):
+ *   x      [B][D]      input logits
+ *   z      [B][D]      final output (= zs[-1]); may be NULL when z_all != NULL
+ *   logdet [B]         sum over layers of sum_j (1-mask_j) s_j; may be NULL
+ *   z_all  [L][B][D]   every layer's output (the reference's zs list); may be NULL */
+int cnf_forward(const cnf_desc* desc, const void* prepared, const float* x, float* z,
+                float* logdet, float* z_all, int64_t B, void* stream);
+
+/* Inverse + log-det (Flow.backward): layers applied L-1..0.
+ *   x_all  [L][B][D]   xs list in the reference's order (x_all[L-1] = input
+ *                       estimate); may be NULL.  logdet = -(forward log-det). */
+int cnf_inverse(const cnf_desc* desc, const void* prepared, const float* z, float* x,
+                float* logdet, float* x_all, int64_t B, void* stream);
+
+/* Loss kinds for cnf_loss_vjp. */
+#define CNF_LOSS_CAL 0  /* -mean(log(softmax(z_L)[y] + 1e-7) + ld)   calibrators.py:287-291 */
+#define CNF_LOSS_CE 1   /* CE(z_L, y) - det * mean(ld)               run_experiment3D.py:107 */
+
+/* Workspace bytes cnf_loss_vjp needs for a batch of B rows. */
+int cnf_vjp_workspace_bytes(const cnf_desc* desc, int64_t B, size_t* bytes);
+
+/* Fused forward + loss + reverse mode.  Writes
+ *   loss_terms[3]   {sum over rows of the per-row loss, sum of ce, sum of ld}
+ *                   (divide by the GLOBAL batch to get the reference's means;
+ *                   the split lets data-parallel ranks all-reduce sums)
+ *   grads           gradient of (sum over THIS batch of the per-row loss) *
+ *                   grad_scale, in cnf_param_count / state_dict order.
+ *                   Overwritten, not accumulated.
+ *   dx [B][D]       d(loss)/dx, may be NULL
+ * Deterministic: no float atomics; fixed-order reductions. */
+int cnf_loss_vjp(const cnf_desc* desc, const void* prepared, const float* x,
+                 const int64_t* y, int32_t loss_kind, float det, float grad_scale,
+                 float* loss_terms, float* grads, float* dx, int64_t B, void* workspace,
+                 size_t workspace_bytes, void* stream);
+
+/* Which kernel family serves this descriptor ("valu-fused", "mfma-tile", ...). */
+const char* cnf_kernel_name(const cnf_desc* desc);
+
+const char* cnf_strerror(int status);
+/* The hipError_t behind the last CNF_ERR_HIP on this thread. */
+int cnf_last_hip_error(void);
+int cnf_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CNF_H_ */

@@ -1,0 +1,102 @@
+"""C-ABI checks that need no GPU: libcnf_hip.so loads, exports every symbol
+include/cnf.h declares, and the host-only entry points validate descriptors."""
+import ctypes
+import os
+import re
+
+import pytest
+import torch
+
+from cnf_hip import _lib
+from cnf_hip.engine import CouplingStack
+from flows.flows import NvpCouplingLayer
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "cnf.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\*?\s+\**(cnf_\w+)\s*\(", src, re.M)))
+
+
+def test_header_and_binding_agree():
+    assert header_functions() == sorted(_lib.EXPORTS)
+
+
+def test_library_exports_every_header_symbol():
+    lib = _lib.lib()
+    for name in header_functions():
+        assert hasattr(lib, name), name
+    assert lib.cnf_abi_version() == _lib.ABI_VERSION
+
+
+def _count(desc):
+    n = ctypes.c_int64()
+    st = _lib.lib().cnf_param_count(ctypes.byref(desc), ctypes.byref(n))
+    return st, n.value
+
+
+def test_param_count_matches_state_dict():
+    for dim, hidden, scale, shift in [(10, [5, 5], 1, 1), (100, [100, 100], 1, 1),
+                                      (3, [5, 5], 0, 1), (10, [], 1, 0), (10, [4, 6, 3], 1, 1)]:
+        layers = [NvpCouplingLayer(dim, hidden, scale=scale, shift=shift) for _ in range(3)]
+        ref = sum(p.numel() for ly in layers for p in ly.parameters() if p.requires_grad)
+        st, n = _count(_lib.make_desc(dim, 3, hidden, scale, shift))
+        assert st == 0 and n == ref
+        stack = CouplingStack(layers)
+        assert stack.param_count() == ref
+        nt = ctypes.c_int32()
+        assert _lib.lib().cnf_param_tensor_count(ctypes.byref(stack.desc), ctypes.byref(nt)) == 0
+        assert nt.value == len(stack.param_tensors())
+
+
+def test_cfg2_param_count_is_1740_and_cfg4_727200():
+    assert _count(_lib.make_desc(10, 6, [5, 5]))[1] == 1740
+    assert _count(_lib.make_desc(100, 12, [100, 100]))[1] == 727200
+
+
+def test_kernel_family_selection():
+    name = lambda d: _lib.lib().cnf_kernel_name(ctypes.byref(d)).decode()
+    assert name(_lib.make_desc(10, 6, [5, 5])) == "valu-fused"
+    assert name(_lib.make_desc(3, 2, [5, 5], scale=0)) == "valu-fused"
+    assert name(_lib.make_desc(100, 12, [100, 100])) == "mfma-tile"
+    assert name(_lib.make_desc(10, 3, [4, 6, 3])) == "mfma-tile"
+
+
+@pytest.mark.parametrize("mutate,status", [
+    (lambda d: setattr(d, "abi_version", 99), -2),
+    (lambda d: setattr(d, "dim", 1), -2),
+    (lambda d: setattr(d, "dim", 1000), -3),
+    (lambda d: setattr(d, "n_layers", 0), -2),
+    (lambda d: setattr(d, "n_hidden", 9), -2),
+    (lambda d: setattr(d, "scale", 2), -2),
+])
+def test_bad_descriptors_are_rejected(mutate, status):
+    d = _lib.make_desc(10, 6, [5, 5])
+    mutate(d)
+    assert _count(d)[0] == status
+    assert _lib.lib().cnf_strerror(status)
+
+
+def test_bad_permutation_rejected():
+    p = torch.full((2, 4), -1, dtype=torch.int64)
+    p[1] = torch.tensor([0, 1, 1, 3])
+    assert _count(_lib.make_desc(4, 2, [3], perms=p))[0] == -2
+    p[1] = torch.tensor([3, 1, 0, 2])
+    assert _count(_lib.make_desc(4, 2, [3], perms=p))[0] == 0
+
+
+def test_forward_argument_validation_without_gpu():
+    lib = _lib.lib()
+    d = _lib.make_desc(10, 6, [5, 5])
+    P = ctypes.c_void_p
+    # B < 0 and NULL pointers are rejected before any device work
+    assert lib.cnf_forward(ctypes.byref(d), P(16), P(16), P(16), P(16), P(0),
+                           ctypes.c_int64(-1), P(0)) == -4
+    assert lib.cnf_forward(ctypes.byref(d), P(0), P(16), P(16), P(16), P(0),
+                           ctypes.c_int64(8), P(0)) == -1
+    assert lib.cnf_forward(ctypes.byref(d), P(16), P(18), P(16), P(16), P(0),
+                           ctypes.c_int64(8), P(0)) == -6
+    # B == 0 is a no-op
+    assert lib.cnf_forward(ctypes.byref(d), P(0), P(0), P(0), P(0), P(0),
+                           ctypes.c_int64(0), P(0)) == 0

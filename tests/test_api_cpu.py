@@ -1,0 +1,79 @@
+"""Drop-in API on host tensors: same init, same state_dict keys, same outputs
+as the reference (golden fixtures)."""
+import numpy as np
+import pytest
+import torch
+
+from _golden import load, names, rel_err
+from _model import build_flow
+from flows.flows import Flow, NvpCouplingLayer
+from flows.realNVP_torch import RealNvpFlow
+from flows.nice_torch import NiceFlow
+
+TOL = 1e-5
+
+
+def test_default_init_reproduces_reference_weights():
+    """Same constructor RNG draws as the reference: seeding gives its weights."""
+    meta, state, d = load("g2_nvp_d10_default")
+    torch.manual_seed(meta["seed"])
+    np.random.seed(meta["seed"])
+    flow = Flow([NvpCouplingLayer(10, [5, 5]) for _ in range(6)])
+    sd = flow.state_dict()
+    assert list(sd.keys()) == [k for k in state.keys()]
+    for k, v in state.items():
+        assert np.array_equal(sd[k].numpy(), v), k
+
+
+def test_random_flip_init_reproduces_reference_perm():
+    meta, state, d = load("g6_d10_randflip")
+    torch.manual_seed(meta["seed"])
+    np.random.seed(meta["seed"])
+    flow = Flow([NvpCouplingLayer(10, [5, 5], random_flip=True) for _ in range(meta["L"])])
+    sd = flow.state_dict()
+    for l in range(meta["L"]):
+        assert np.array_equal(sd["layers.%d.perm" % l].numpy(), state["layers.%d.perm" % l])
+        assert np.array_equal(sd["layers.%d.rev_perm" % l].numpy(),
+                              state["layers.%d.rev_perm" % l])
+
+
+@pytest.mark.parametrize("name", [n for n in names() if not n.startswith("g5")])
+def test_cpu_forward_inverse_match_reference(name):
+    meta, state, d = load(name)
+    flow = build_flow(meta, state)
+    with torch.no_grad():
+        zs, ld = flow(torch.from_numpy(d["x"]))
+    assert len(zs) == meta["L"]
+    assert rel_err(torch.stack(zs).numpy(), d["zs"]) <= TOL
+    assert tuple(ld.shape) == d["ld"].shape
+    assert rel_err(ld.numpy(), d["ld"]) <= TOL
+    if "inv_xs" in d:
+        with torch.no_grad():
+            xs, ild = flow.backward(torch.from_numpy(d["zs"][-1]))
+        got = torch.stack(xs).numpy()
+        if d["inv_xs"].shape[0] == 1:
+            got = got[-1:]
+        assert rel_err(got, d["inv_xs"]) <= TOL
+        assert rel_err(ild.numpy(), d["inv_ld"]) <= TOL
+
+
+def test_factories_return_final_output_and_ignore_calibrator_kwargs():
+    torch.manual_seed(0)
+    f = RealNvpFlow(3, layers=5, hidden_size=[3, 3], dev="cpu", epochs=10, batch_size=7)
+    x = torch.randn(8, 3)
+    z, ld = f(x)
+    zs, ld2 = f.forward_all(x)
+    assert torch.equal(z, zs[-1]) and torch.equal(ld, ld2)
+    xr, ild = f.backward(z)
+    assert torch.allclose(xr, x, atol=1e-5) and torch.allclose(ild, -ld, atol=1e-6)
+    n = NiceFlow(3, layers=2, hidden_size=[5, 5])
+    z, ld = n(x)
+    assert torch.count_nonzero(ld) == 0
+    assert sum(1 for k in n.state_dict() if ".s." in k) == 0
+
+
+def test_noninvertible_flow_raises():
+    from flows.flows import PlanarLayer
+    f = Flow([PlanarLayer(3), NvpCouplingLayer(3)])
+    with pytest.raises(ValueError, match="Flow inverse not tractable!"):
+        f.backward(torch.randn(4, 3))

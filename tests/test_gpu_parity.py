@@ -1,0 +1,172 @@
+"""Parity of the HIP path (through the C ABI) with the reference.
+
+Small cases: against the golden fixtures (outputs of the reference's own
+flows/flows.py).  Full BASELINE sizes: against the numpy oracle on sampled rows
+plus size-independent properties (round trip, log-det antisymmetry,
+determinism, final-only == all-layers).  Tolerance: the north_star's 1e-5 under
+SURVEY 8(c)'s metric max|a-b|/(|ref|+1).
+"""
+import numpy as np
+import pytest
+import torch
+
+from _golden import load, names, rel_err
+from _model import build_flow
+from cnf_hip import engine
+from flows.flows import Flow, NvpCouplingLayer
+from oracle import cnf_oracle as O
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    assert torch.cuda.is_available(), "GPU tests need a ROCm device"
+    yield
+
+
+def _oracle_layers(flow):
+    l0 = flow.layers[0]
+    st = {k: v.detach().cpu().numpy() for k, v in flow.state_dict().items()}
+    return O.layers_from_state(st, len(flow.layers), l0.dim, len(l0.hidden_size) + 1,
+                               l0.scale, l0.shift)
+
+
+CASES = [n for n in names() if not n.startswith("g5")]
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_forward_matches_reference_fixture(name):
+    meta, state, d = load(name)
+    strict = name == "g6_d4_nan"
+    flow = build_flow(meta, state, DEV, strict_nan=strict)
+    x = torch.from_numpy(d["x"]).to(DEV)
+    n0 = engine.stats["forward"]
+    with torch.no_grad():
+        zs, ld = flow(x)
+    torch.cuda.synchronize()
+    assert engine.stats["forward"] == n0 + 1, "native cnf_forward did not run"
+    assert len(zs) == meta["L"]
+    assert rel_err(torch.stack(zs).cpu().numpy(), d["zs"]) <= TOL
+    assert tuple(ld.shape) == d["ld"].shape
+    assert rel_err(ld.cpu().numpy(), d["ld"]) <= TOL
+    with torch.no_grad():
+        z, ld2 = flow.transform(x)
+    assert torch.equal(z, zs[-1]) and torch.equal(ld2, ld)
+
+
+@pytest.mark.parametrize("name", [n for n in CASES if n != "g6_d4_nan"])
+def test_inverse_matches_reference_fixture(name):
+    meta, state, d = load(name)
+    if "inv_xs" not in d:
+        pytest.skip("no inverse recorded")
+    flow = build_flow(meta, state, DEV)
+    z = torch.from_numpy(d["zs"][-1]).to(DEV)
+    n0 = engine.stats["inverse"]
+    with torch.no_grad():
+        xs, ld = flow.backward(z)
+    assert engine.stats["inverse"] == n0 + 1, "native cnf_inverse did not run"
+    got = torch.stack(xs).cpu().numpy()
+    if d["inv_xs"].shape[0] == 1:
+        got = got[-1:]
+    assert rel_err(got, d["inv_xs"]) <= TOL
+    assert rel_err(ld.cpu().numpy(), d["inv_ld"]) <= TOL
+
+
+def test_fast_mode_on_overflow_case_differs_only_at_reference_nans():
+    meta, state, d = load("g6_d4_nan")
+    flow = build_flow(meta, state, DEV, strict_nan=False)
+    with torch.no_grad():
+        zs, ld = flow(torch.from_numpy(d["x"]).to(DEV))
+    got = torch.stack(zs).cpu().numpy()
+    ok = ~np.isnan(d["zs"])
+    assert np.isnan(d["zs"]).any()
+    assert rel_err(got[ok], d["zs"][ok]) <= TOL
+
+
+def test_single_layer_calls_are_native():
+    meta, state, d = load("g2_nvp_d10_n01")
+    flow = build_flow(meta, state, DEV)
+    x = torch.from_numpy(d["x"]).to(DEV)
+    n0 = engine.stats["forward"]
+    with torch.no_grad():
+        z1, ld1 = flow.layers[0](x)
+        xb, ldb = flow.layers[0].backward(z1)
+    assert engine.stats["forward"] == n0 + 1
+    assert rel_err(z1.cpu().numpy(), d["zs"][0]) <= TOL
+    assert rel_err(xb.cpu().numpy(), d["x"]) <= TOL
+    assert torch.allclose(ldb, -ld1, atol=1e-6)
+
+
+def _make_flow(D, L, hidden, sigma, seed, random_flip=False, scale=True):
+    torch.manual_seed(seed)
+    np.random.seed(seed)
+    f = Flow([NvpCouplingLayer(D, hidden, scale=scale, random_flip=random_flip)
+              for _ in range(L)])
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for p in f.parameters():
+            if p.requires_grad:
+                p.copy_(torch.randn(p.shape, generator=g) * sigma)
+    return f.to(DEV)
+
+
+def _logits(B, D, seed):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    x = torch.randn(B, D, device=DEV, generator=g)
+    y = torch.randint(0, D, (B,), device=DEV, generator=g)
+    x[torch.arange(B, device=DEV), y] += 2.0
+    return x - x.mean(dim=1, keepdim=True)
+
+
+@pytest.mark.parametrize("D,L,hidden,B,sigma,flip", [
+    (10, 6, [5, 5], 1 << 20, 0.1, False),        # cfg2 / cfg5 at full size
+    (10, 6, [5, 5], 1000003, 0.2, True),         # ragged batch, random_flip
+    (3, 2, [5, 5], 1 << 20, 0.2, False),         # cfg1 shape, RealNVP
+    (100, 12, [100, 100], 1 << 16, 0.03, False), # cfg4
+])
+def test_full_size_properties(D, L, hidden, B, sigma, flip):
+    flow = _make_flow(D, L, hidden, sigma, 5, random_flip=flip)
+    x = _logits(B, D, 7)
+    with torch.no_grad():
+        z, ld = flow.transform(x)
+        z2, ld2 = flow.transform(x)
+        xr, ild = flow.inverse_transform(z)
+    assert torch.equal(z, z2) and torch.equal(ld, ld2), "non-deterministic"
+    err = ((xr - x).abs() / (x.abs() + 1)).max().item()
+    assert err <= TOL, err
+    assert ((ild + ld).abs() / (ld.abs() + 1)).max().item() <= TOL
+    # sampled rows against the numpy oracle
+    idx = torch.randperm(B, generator=torch.Generator().manual_seed(1))[:2048].to(DEV)
+    xs = x[idx].cpu().numpy()
+    ol = _oracle_layers(flow)
+    if flip:
+        for l, ly in enumerate(flow.layers):
+            ol[l] = O.OracleLayer(D, ol[l].s_net, ol[l].t_net, ly.perm.reshape(-1).cpu().numpy())
+    ozs, old = O.flow_forward(ol, xs)
+    assert rel_err(z[idx].cpu().numpy(), ozs[-1]) <= TOL
+    assert rel_err(ld[idx].cpu().numpy(), old) <= TOL
+
+
+def test_edge_batches():
+    flow = _make_flow(10, 6, [5, 5], 0.2, 3)
+    for B in (0, 1, 2, 63, 255, 257):
+        x = _logits(max(B, 1), 10, B)[:B]
+        with torch.no_grad():
+            zs, ld = flow(x)
+        ol = _oracle_layers(flow)
+        ozs, old = O.flow_forward(ol, x.cpu().numpy())
+        assert rel_err(torch.stack(zs).cpu().numpy(), np.stack(ozs)) <= TOL
+        assert ld.shape == (torch.Size([]) if B == 1 else torch.Size([B]))
+
+
+def test_nonaligned_input_view():
+    flow = _make_flow(10, 6, [5, 5], 0.2, 4)
+    big = _logits(4097, 10, 2)
+    x = big.view(-1)[3:3 + 4096 * 10].view(4096, 10)   # 12-byte offset: scalar I/O path
+    with torch.no_grad():
+        z, ld = flow.transform(x)
+    ozs, old = O.flow_forward(_oracle_layers(flow), x.cpu().numpy())
+    assert rel_err(z.cpu().numpy(), ozs[-1]) <= TOL
