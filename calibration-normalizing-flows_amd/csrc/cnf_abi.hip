@@ -57,6 +57,14 @@ int derive_shape(const cnf_desc* d, Shape* s) {
   s->valu_id = s->D <= 16 ? valu_supported(*s) : -1;
   if (s->valu_id >= 0) {
     s->family = Family::kValu;
+    int64_t off = 0;
+    for (int i = 0; i < s->n_lin; ++i) {
+      const int nin = i == 0 ? s->DC : s->units[i];
+      const int nout = s->units[i + 1];
+      s->valu_lin_off[i] = off;
+      off += ((int64_t)nout * ((nin + 3) & ~3) + ((nout + 3) & ~3) + 15) & ~15;
+    }
+    s->valu_net_floats = off;
   } else {
     s->family = Family::kTile;
     int st = tile_configure(s);
@@ -111,8 +119,10 @@ int cnf_prepared_bytes(const cnf_desc* desc, size_t* bytes) {
   int st = derive_shape(desc, &s);
   if (st != CNF_OK) return st;
   if (!bytes) return CNF_ERR_NULL;
-  const int64_t wf = s.family == Family::kTile ? s.tile_layer_floats * s.L : s.layer_floats * s.L;
-  *bytes = (size_t)(idx_bytes(s) + wf * 4);
+  const int64_t wf = s.family == Family::kTile ? s.tile_layer_floats * s.L
+                                                : s.valu_net_floats * s.nets * s.L;
+  // +256: scalar-cache prefetch reads whole 64-B lines past the last weight
+  *bytes = (size_t)(idx_bytes(s) + wf * 4 + 256);
   return CNF_OK;
 }
 

@@ -31,6 +31,9 @@ struct Shape {
   const int64_t* perms_host = nullptr;  // desc->perms (valid during the call)
   Family family = Family::kTile;
   int valu_id = -1;                  // index into the VALU instantiation table
+  // VALU compact layout (cnf_valu_common.h): per Linear W[nout][pad4(nin)], b[pad4(nout)]
+  int64_t valu_lin_off[kMaxLin] = {};
+  int64_t valu_net_floats = 0;
   // tile (MFMA) layout
   int NO = 0;                        // last-linear outputs computed: DT (fast) or D (strict)
   int lin_nin[kMaxLin] = {}, lin_nout[kMaxLin] = {}, lin_inoff[kMaxLin] = {};

@@ -228,7 +228,7 @@ struct PrepSeg {
   const float* W;
   const float* b;
   int64_t dst;  // float offset in the weights region
-  int mode;     // 0: natural copy (W then b), 1: MFMA tiles
+  int mode;     // 0: natural copy (W then b), 1: MFMA tiles, 2: compact (VALU)
   int nout_full, nin_full, in_off, nin, nout, OT, KS;
 };
 
@@ -254,6 +254,21 @@ __global__ void k_prepare(PrepArgs a, float* __restrict__ wreg, int32_t* __restr
     const int64_t nW = (int64_t)g.nout_full * g.nin_full;
     for (int64_t i = threadIdx.x; i < nW + g.nout_full; i += blockDim.x)
       dst[i] = i < nW ? g.W[i] : g.b[i - nW];
+    return;
+  }
+  if (g.mode == 2) {
+    const int S = (g.nin + 3) & ~3, NP = (g.nout_full + 3) & ~3;
+    const int64_t nW = (int64_t)g.nout_full * S;
+    for (int64_t i = threadIdx.x; i < nW + NP; i += blockDim.x) {
+      float v = 0.f;
+      if (i < nW) {
+        const int o = (int)(i / S), k = (int)(i - (int64_t)o * S);
+        if (k < g.nin) v = g.W[(int64_t)o * g.nin_full + g.in_off + k];
+      } else if (i - nW < g.nout_full) {
+        v = g.b[i - nW];
+      }
+      dst[i] = v;
+    }
     return;
   }
   for (int o = threadIdx.x; o < g.OT * 16; o += blockDim.x) dst[o] = o < g.nout ? g.b[o] : 0.f;
@@ -337,7 +352,8 @@ int prepare_run(const Shape& s, const float* const* params, void* prepared, hipS
     a.D = s.D;
     a.L = s.L;
     a.nseg = 0;
-    int64_t dst = tiled ? (int64_t)l * s.tile_layer_floats : (int64_t)l * s.layer_floats;
+    int64_t dst = tiled ? (int64_t)l * s.tile_layer_floats
+                        : (int64_t)l * s.valu_net_floats * s.nets;
     for (int net = 0; net < s.nets; ++net) {
       for (int i = 0; i < s.n_lin; ++i) {
         PrepSeg& g = a.seg[a.nseg++];
@@ -355,12 +371,14 @@ int prepare_run(const Shape& s, const float* const* params, void* prepared, hipS
           g.KS = s.lin_KS[i];
           g.dst = dst + s.tile_lin_off[i];
         } else {
-          g.mode = 0;
-          g.dst = dst;
-          dst += (int64_t)g.nout_full * g.nin_full + g.nout_full;
+          g.mode = 2;
+          g.in_off = i == 0 ? s.DT : 0;
+          g.nin = i == 0 ? s.DC : g.nin_full;
+          g.nout = g.nout_full;
+          g.dst = dst + s.valu_lin_off[i];
         }
       }
-      if (tiled) dst += s.tile_net_floats;
+      dst += tiled ? s.tile_net_floats : s.valu_net_floats;
     }
     const int64_t* perm = nullptr;
     if (s.any_perm && s.perms_host) {

@@ -22,131 +22,65 @@
 // and stores are 16-byte-per-lane coalesced sweeps of the block's tile.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+#include <mutex>
+#include <type_traits>
+#include <unordered_map>
+
 #include "cnf_internal.h"
+#include "cnf_valu_common.h"
 
 namespace cnf {
 namespace {
 
-constexpr int kRows = 256;  // rows (= threads) per block
+using namespace valu;
 
-template <bool STRICT>
-__device__ __forceinline__ float relu(float a) {
-  // torch.relu propagates NaN; v_max_f32 (IEEE maxNum) would drop it.
-  if constexpr (STRICT) return a < 0.f ? 0.f : a;
-  else return fmaxf(a, 0.f);
-}
-
-// y[o] = b[o] (+p0) + sum_k W[o][OFF+k] * x[k],  o < NOUT, W is [NOUTF][NINF].
-template <int NINF, int OFF, int NIN, int NOUTF, int NOUT, bool RELU, bool STRICT, bool POISON>
-__device__ __forceinline__ void linear(const float* __restrict__ w, const float* x, float* y,
-                                       float p0) {
-  const float* __restrict__ b = w + NOUTF * NINF;
-#pragma unroll
-  for (int o = 0; o < NOUT; ++o) {
-    float a = b[o];
-    if constexpr (POISON) a += p0;
-#pragma unroll
-    for (int k = 0; k < NIN; ++k) a = fmaf(w[o * NINF + OFF + k], x[k], a);
-    y[o] = RELU ? relu<STRICT>(a) : a;
-  }
-}
-
-template <int D, int H1, int H2>
-struct Net {
-  static constexpr int DT = D / 2, DC = D - D / 2;
-  static constexpr int floats = H1 == 0   ? D * D + D
-                                : H2 == 0 ? H1 * D + H1 + D * H1 + D
-                                          : H1 * D + H1 + H2 * H1 + H2 + D * H2 + D;
-};
-
-// Conditioner MLP on the conditioning half c[DC] (the masked input x_b has
-// zeros at the DT transformed positions, so their weight columns drop out).
-template <int D, int H1, int H2, int NO, bool STRICT>
-__device__ __forceinline__ void mlp(const float* __restrict__ w, const float* c, float p0,
-                                    float* o) {
-  constexpr int DT = D / 2, DC = D - D / 2;
-  if constexpr (H1 == 0) {
-    linear<D, DT, DC, D, NO, false, STRICT, STRICT>(w, c, o, p0);
-  } else if constexpr (H2 == 0) {
-    float h1[H1];
-    linear<D, DT, DC, H1, H1, true, STRICT, STRICT>(w, c, h1, p0);
-    linear<H1, 0, H1, D, NO, false, STRICT, false>(w + H1 * D + H1, h1, o, 0.f);
-  } else {
-    float h1[H1], h2[H2];
-    linear<D, DT, DC, H1, H1, true, STRICT, STRICT>(w, c, h1, p0);
-    const float* w2 = w + H1 * D + H1;
-    linear<H1, 0, H1, H2, H2, true, STRICT, false>(w2, h1, h2, 0.f);
-    linear<H2, 0, H2, D, NO, false, STRICT, false>(w2 + H2 * H1 + H2, h2, o, 0.f);
-  }
-}
-
-// Register holding logical position j in orientation O (O: row stored reversed).
-template <int D, bool O>
-__device__ __forceinline__ constexpr int R(int j) { return O ? D - 1 - j : j; }
-
-template <int D>
-__device__ __forceinline__ float pick(const float* v, int idx) {
-  float r = v[0];
-#pragma unroll
-  for (int k = 1; k < D; ++k) r = (idx == k) ? v[k] : r;
-  return r;
-}
-
-// Gather v (orientation O) into orientation !O through the layer's uniform
-// index table: new logical j takes old logical q[j].
-template <int D, bool O>
-__device__ __forceinline__ void permute(float* v, const int32_t* __restrict__ q) {
-  float nv[D];
-#pragma unroll
-  for (int j = 0; j < D; ++j) nv[R<D, !O>(j)] = pick<D>(v, R<D, O>(q[j]));
-#pragma unroll
-  for (int k = 0; k < D; ++k) v[k] = nv[k];
-}
 
 // One coupling layer, input in orientation O, output in orientation !O.
-template <int D, int H1, int H2, bool INV, bool STRICT, bool O>
-__device__ __forceinline__ void step(float* v, float& ld, const float* __restrict__ wl,
-                                     int scale, int shift, int net_floats, bool perm,
+template <int D, int H1, int H2, bool INV, bool STRICT, bool O, bool FX, bool CH, class T>
+__device__ __forceinline__ void step(T* v, T& ld, const float* __restrict__ wl, int scale,
+                                     int shift, int net_floats, bool perm,
                                      const int32_t* __restrict__ q) {
   constexpr int DT = D / 2, DC = D - D / 2;
   constexpr int NO = STRICT ? D : DT;
+  const T zero = splat(0.f, T{});
   // Inverse: flip (+rev_perm) BEFORE the coupling (flows/flows.py:115-117).
   constexpr bool OC = INV ? !O : O;  // orientation the coupling sees
   if constexpr (INV) {
     if (perm) permute<D, O>(v, q);
   }
-  float c[DC];
+  T c[DC];
 #pragma unroll
   for (int k = 0; k < DC; ++k) c[k] = v[R<D, OC>(DT + k)];
-  float p0 = 0.f;
+  T p0 = zero;
   if constexpr (STRICT) {
     // x_b = mask*x: a non-finite transformed input makes 0*x = NaN feed both nets.
 #pragma unroll
     for (int j = 0; j < DT; ++j) p0 += 0.f * v[R<D, OC>(j)];
   }
-  float s[NO], t[NO];
+  T s[NO], t[NO];
   if (scale) {
-    mlp<D, H1, H2, NO, STRICT>(wl, c, p0, s);
+    mlp<D, H1, H2, NO, STRICT, CH>(wl, c, p0, s);
     wl += net_floats;
   } else {
 #pragma unroll
-    for (int j = 0; j < NO; ++j) s[j] = 0.f;
+    for (int j = 0; j < NO; ++j) s[j] = zero;
   }
   if (shift) {
-    mlp<D, H1, H2, NO, STRICT>(wl, c, p0, t);
+    mlp<D, H1, H2, NO, STRICT, CH>(wl, c, p0, t);
   } else {
 #pragma unroll
-    for (int j = 0; j < NO; ++j) t[j] = 0.f;
+    for (int j = 0; j < NO; ++j) t[j] = zero;
   }
 #pragma unroll
   for (int j = 0; j < DT; ++j) {
-    float& x = v[R<D, OC>(j)];
+    T& x = v[R<D, OC>(j)];
     if constexpr (!INV) {
-      float y = fmaf(x, expf(s[j]), t[j]);
+      T y = fmaV(x, expT<FX>(s[j]), t[j]);
       x = STRICT ? 0.f * x + y : y;
       ld += s[j];
     } else {
-      float y = (x - t[j]) * expf(-s[j]);
+      T y = (x - t[j]) * expT<FX>(-s[j]);
       x = STRICT ? 0.f * x + y : y;
       ld -= s[j];
     }
@@ -155,8 +89,8 @@ __device__ __forceinline__ void step(float* v, float& ld, const float* __restric
     // masked positions: x + 0*(x*exp(s)+t) is NaN when exp(s) overflows.
 #pragma unroll
     for (int j = DT; j < D; ++j) {
-      float& x = v[R<D, OC>(j)];
-      float y = INV ? (x - t[j]) * expf(-s[j]) : fmaf(x, expf(s[j]), t[j]);
+      T& x = v[R<D, OC>(j)];
+      T y = INV ? (x - t[j]) * expT<false>(-s[j]) : fmaV(x, expT<false>(s[j]), t[j]);
       x = x + 0.f * y;
       ld += 0.f * s[j];
     }
@@ -167,6 +101,16 @@ __device__ __forceinline__ void step(float* v, float& ld, const float* __restric
   }
 }
 
+// Block barrier for LDS hand-offs only: waits for this wave's LDS traffic,
+// not for its outstanding global loads/stores (a __syncthreads() would also
+// drain vmcnt, serialising the prefetch and the output stores).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int ROWS>
 __device__ __forceinline__ void tile_load(float* __restrict__ sm, const float* __restrict__ src,
                                           int n, bool vec) {
   const int tid = threadIdx.x;
@@ -175,12 +119,13 @@ __device__ __forceinline__ void tile_load(float* __restrict__ sm, const float* _
     const int n4 = n >> 2;
     const float4* s4 = reinterpret_cast<const float4*>(src);
     float4* d4 = reinterpret_cast<float4*>(sm);
-    for (int i = tid; i < n4; i += kRows) d4[i] = s4[i];
+    for (int i = tid; i < n4; i += ROWS) d4[i] = s4[i];
     done = n4 << 2;
   }
-  for (int i = done + tid; i < n; i += kRows) sm[i] = src[i];
+  for (int i = done + tid; i < n; i += ROWS) sm[i] = src[i];
 }
 
+template <int ROWS>
 __device__ __forceinline__ void tile_store(float* __restrict__ dst, const float* __restrict__ sm,
                                            int n, bool vec) {
   const int tid = threadIdx.x;
@@ -189,73 +134,182 @@ __device__ __forceinline__ void tile_store(float* __restrict__ dst, const float*
     const int n4 = n >> 2;
     float4* d4 = reinterpret_cast<float4*>(dst);
     const float4* s4 = reinterpret_cast<const float4*>(sm);
-    for (int i = tid; i < n4; i += kRows) d4[i] = s4[i];
+    for (int i = tid; i < n4; i += ROWS) d4[i] = s4[i];
     done = n4 << 2;
   }
-  for (int i = done + tid; i < n; i += kRows) dst[i] = sm[i];
+  for (int i = done + tid; i < n; i += ROWS) dst[i] = sm[i];
 }
 
-// Write the block's rows (registers in orientation O) to dst through LDS.
-template <int D, bool O>
-__device__ __forceinline__ void store_rows(float* __restrict__ dst, float* sm, const float* v,
+// lane value <-> the RW rows a thread owns (rows tid and tid + ROWS of the tile)
+template <int ROWS>
+__device__ __forceinline__ float get_row(const float* sm, int i, int D, int k, float) {
+  return sm[i * D + k];
+}
+template <int ROWS, class V>
+__device__ __forceinline__ V get_row(const float* sm, int i, int D, int k, V) {
+  V r;
+#pragma unroll
+  for (int q = 0; q < (int)(sizeof(V) / sizeof(float)); ++q) r[q] = sm[(i + q * ROWS) * D + k];
+  return r;
+}
+template <int ROWS>
+__device__ __forceinline__ void put_row(float* sm, int i, int D, int k, float v) {
+  sm[i * D + k] = v;
+}
+template <int ROWS, class V>
+__device__ __forceinline__ void put_row(float* sm, int i, int D, int k, V v) {
+#pragma unroll
+  for (int q = 0; q < (int)(sizeof(V) / sizeof(float)); ++q) sm[(i + q * ROWS) * D + k] = v[q];
+}
+
+// Write the tile's rows (registers in orientation O) to dst through LDS.
+template <int D, int ROWS, bool O, class T>
+__device__ __forceinline__ void store_rows(float* __restrict__ dst, float* sm, const T* v,
                                            int nrows, bool vec) {
   const int tid = threadIdx.x;
-  __syncthreads();  // previous users of sm are done
-  if (tid < nrows) {
+  lds_barrier();  // previous users of sm are done
 #pragma unroll
-    for (int j = 0; j < D; ++j) sm[tid * D + j] = v[R<D, O>(j)];
-  }
-  __syncthreads();
-  tile_store(dst, sm, nrows * D, vec);
+  for (int j = 0; j < D; ++j) put_row<ROWS>(sm, tid, D, j, v[R<D, O>(j)]);
+  lds_barrier();
+  tile_store<ROWS>(dst, sm, nrows * D, vec);
 }
 
-template <int D, int H1, int H2, bool INV, bool STRICT>
-__global__ __launch_bounds__(kRows) void k_valu(
-    const float* __restrict__ W, const int32_t* __restrict__ qtab,
+template <int ROWS>
+__device__ __forceinline__ void store_ld(float* ld_out, int64_t row0, int tid, int nrows, float v) {
+  if (tid < nrows) ld_out[row0 + tid] = v;
+}
+template <int ROWS, class V>
+__device__ __forceinline__ void store_ld(float* ld_out, int64_t row0, int tid, int nrows, V v) {
+#pragma unroll
+  for (int q = 0; q < (int)(sizeof(V) / sizeof(float)); ++q)
+    if (tid + q * ROWS < nrows) ld_out[row0 + tid + q * ROWS] = v[q];
+}
+
+// Fused L-layer coupling pass.  One block = ROWS threads = ROWS*RW logit
+// vectors per tile.  PERSIST: a grid of (CUs x resident blocks) walks the
+// tiles, prefetching the next tile's input into registers (16-B loads) while
+// the current tile computes.
+template <int D, int H1, int H2, bool INV, bool STRICT, int RW, int ROWS, bool PERSIST, int WPE,
+          bool FX, bool WL, bool WU = false, bool CH = false>
+__global__ __launch_bounds__(ROWS, WPE) void k_valu(
+    const float* __restrict__ Wg, const int32_t* __restrict__ qtab,
     const int32_t* __restrict__ lflag, const float* __restrict__ in, float* __restrict__ out,
     float* __restrict__ ld_out, float* __restrict__ all, int64_t B, int L, int scale, int shift,
     int any_perm, int vec_io) {
-  __shared__ __attribute__((aligned(16))) float sm[kRows * D];
+  using T = typename RowT<RW>::type;
+  constexpr int TR = ROWS * RW;  // rows per tile
+  constexpr int TF = TR * D;     // floats per tile
+  constexpr int NPT = (TF / 4 + ROWS - 1) / ROWS;  // prefetched float4 per thread
+  // ONE dynamic LDS array: [tile: TF floats][weights (WL): L * layer_floats]
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* sm = smem;
   const int tid = threadIdx.x;
-  const int64_t row0 = (int64_t)blockIdx.x * kRows;
-  const int nrows = (int)((B - row0) < kRows ? (B - row0) : kRows);
   const bool vec = vec_io != 0;
   constexpr int NF = Net<D, H1, H2>::floats;
   const int layer_floats = (scale + shift) * NF;
+  const float* W = Wg;
+  if constexpr (WL) {
+    // the whole weight blob, once per block, in one round trip of 16-B loads
+    float* wl = smem + TF;
+    const int n4 = (L * layer_floats) >> 2;  // layer_floats % 4 == 0 (compact layout)
+    const float4* s4 = reinterpret_cast<const float4*>(Wg);
+    float4* d4 = reinterpret_cast<float4*>(wl);
+    for (int i = tid; i < n4; i += ROWS) d4[i] = s4[i];
+    lds_barrier();
+    W = wl;
+  }
+  const int64_t ntiles = (B + TR - 1) / TR;
+  const int64_t nfull = B / TR;  // tiles whose TF floats are all in range
+  const int64_t stride = PERSIST ? (int64_t)gridDim.x : ntiles;
 
-  tile_load(sm, in + row0 * D, nrows * D, vec);
-  __syncthreads();
-  float v[D];
+  float4 pf[PERSIST ? NPT : 1];
+  auto prefetch = [&](int64_t t) {
+    const float4* s4 = reinterpret_cast<const float4*>(in + t * TF);
 #pragma unroll
-  for (int k = 0; k < D; ++k) v[k] = tid < nrows ? sm[tid * D + k] : 0.f;
+    for (int i = 0; i < NPT; ++i) {
+      const int k = i * ROWS + tid;
+      if (k < TF / 4) pf[i] = s4[k];
+    }
+  };
+  // WU: pull the weight blob into this XCD's L2 with one round trip of
+  // vector loads, issued beside the first tile's input loads, so the first
+  // waves' scalar-cache misses hit L2 instead of going to memory one Linear
+  // at a time (the caches start cold at every dispatch).
+  float4 wu[WU ? 4 : 1];
+  constexpr int kWU = WU ? 4 : 0;
+  if constexpr (WU) {
+    const float4* s4 = reinterpret_cast<const float4*>(Wg);
+    const int n4 = (L * layer_floats) >> 2;
+#pragma unroll
+    for (int i = 0; i < kWU; ++i) {
+      const int k = tid + i * ROWS;
+      wu[i] = k < n4 ? s4[k] : float4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  int64_t tile = blockIdx.x;
+  if constexpr (PERSIST) {
+    if (vec && tile < nfull) prefetch(tile);
+  }
 
-  float ld = 0.f;
-  // step index i = 0..L-1; layer = i (forward) or L-1-i (inverse)
-  auto layer_of = [&](int i) { return INV ? L - 1 - i : i; };
-  int i = 0;
-  for (; i + 1 < L; i += 2) {
-    int la = layer_of(i), lb = layer_of(i + 1);
-    bool pa = any_perm && (lflag[la] & kFlagPerm), pb = any_perm && (lflag[lb] & kFlagPerm);
-    step<D, H1, H2, INV, STRICT, false>(v, ld, W + (int64_t)la * layer_floats, scale, shift, NF,
-                                        pa, qtab + la * D);
-    if (all) store_rows<D, true>(all + (int64_t)i * B * D + row0 * D, sm, v, nrows, vec);
-    step<D, H1, H2, INV, STRICT, true>(v, ld, W + (int64_t)lb * layer_floats, scale, shift, NF,
-                                       pb, qtab + lb * D);
-    if (all) store_rows<D, false>(all + (int64_t)(i + 1) * B * D + row0 * D, sm, v, nrows, vec);
+  for (; tile < ntiles; tile += stride) {
+    const int64_t row0 = tile * TR;
+    const int nrows = (int)((B - row0) < TR ? (B - row0) : TR);
+    lds_barrier();  // previous tile is done with sm
+    bool from_regs = false;
+    if constexpr (PERSIST) from_regs = vec && tile < nfull;
+    if (from_regs) {
+      float4* d4 = reinterpret_cast<float4*>(sm);
+#pragma unroll
+      for (int i = 0; i < NPT; ++i) {
+        const int k = i * ROWS + tid;
+        if (k < TF / 4) d4[k] = pf[i];
+      }
+    } else {
+      tile_load<ROWS>(sm, in + row0 * D, nrows * D, vec);
+    }
+    lds_barrier();
+    if constexpr (PERSIST) {
+      const int64_t nt = tile + stride;
+      if (vec && nt < nfull) prefetch(nt);  // lands while this tile computes
+    }
+    if constexpr (WU) {
+#pragma unroll
+      for (int i = 0; i < kWU; ++i) asm volatile("" ::"v"(wu[i].x));
+    }
+    // rows past the batch end read stale LDS: harmless, never stored
+    T v[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) v[k] = get_row<ROWS>(sm, tid, D, k, T{});
+
+    T ld = splat(0.f, T{});
+    // step index i = 0..L-1; layer = i (forward) or L-1-i (inverse)
+    auto layer_of = [&](int i) { return INV ? L - 1 - i : i; };
+    int i = 0;
+    for (; i + 1 < L; i += 2) {
+      int la = layer_of(i), lb = layer_of(i + 1);
+      bool pa = any_perm && (lflag[la] & kFlagPerm), pb = any_perm && (lflag[lb] & kFlagPerm);
+      step<D, H1, H2, INV, STRICT, false, FX && !STRICT, CH && !WL>(v, ld, W + (int64_t)la * layer_floats, scale, shift,
+                                          NF, pa, qtab + la * D);
+      if (all) store_rows<D, ROWS, true>(all + (int64_t)i * B * D + row0 * D, sm, v, nrows, vec);
+      step<D, H1, H2, INV, STRICT, true, FX && !STRICT, CH && !WL>(v, ld, W + (int64_t)lb * layer_floats, scale, shift,
+                                         NF, pb, qtab + lb * D);
+      if (all)
+        store_rows<D, ROWS, false>(all + (int64_t)(i + 1) * B * D + row0 * D, sm, v, nrows, vec);
+    }
+    bool odd = i < L;
+    if (odd) {
+      int la = layer_of(i);
+      bool pa = any_perm && (lflag[la] & kFlagPerm);
+      step<D, H1, H2, INV, STRICT, false, FX && !STRICT, CH && !WL>(v, ld, W + (int64_t)la * layer_floats, scale, shift,
+                                          NF, pa, qtab + la * D);
+      if (all) store_rows<D, ROWS, true>(all + (int64_t)i * B * D + row0 * D, sm, v, nrows, vec);
+    }
+    if (out) {
+      if (odd) store_rows<D, ROWS, true>(out + row0 * D, sm, v, nrows, vec);
+      else store_rows<D, ROWS, false>(out + row0 * D, sm, v, nrows, vec);
+    }
+    if (ld_out) store_ld<ROWS>(ld_out, row0, tid, nrows, ld);
   }
-  bool odd = i < L;
-  if (odd) {
-    int la = layer_of(i);
-    bool pa = any_perm && (lflag[la] & kFlagPerm);
-    step<D, H1, H2, INV, STRICT, false>(v, ld, W + (int64_t)la * layer_floats, scale, shift, NF,
-                                        pa, qtab + la * D);
-    if (all) store_rows<D, true>(all + (int64_t)i * B * D + row0 * D, sm, v, nrows, vec);
-  }
-  if (out) {
-    if (odd) store_rows<D, true>(out + row0 * D, sm, v, nrows, vec);
-    else store_rows<D, false>(out + row0 * D, sm, v, nrows, vec);
-  }
-  if (ld_out && tid < nrows) ld_out[row0 + tid] = ld;
 }
 
 // ---------------------------------------------------------------------------
@@ -264,15 +318,39 @@ __global__ __launch_bounds__(kRows) void k_valu(
 using KFn = void (*)(const float*, const int32_t*, const int32_t*, const float*, float*, float*,
                      float*, int64_t, int, int, int, int, int);
 
-struct Entry {
-  int D, H1, H2;
+struct Variant {
   KFn fn[2][2];  // [inverse][strict]
+  int rw, rows, persist, wl;
 };
 
-#define CNF_VALU(D, H1, H2)                                                             \
-  {D, H1, H2,                                                                           \
-   {{k_valu<D, H1, H2, false, false>, k_valu<D, H1, H2, false, true>},                  \
-    {k_valu<D, H1, H2, true, false>, k_valu<D, H1, H2, true, true>}}}
+#define CNF_VARIANT_X(D, H1, H2, RW, ROWS, P, WPE, FX, WL, WU, CH)                        \
+  {{{k_valu<D, H1, H2, false, false, RW, ROWS, P, WPE, FX, WL, WU, CH>,                    \
+     k_valu<D, H1, H2, false, true, RW, ROWS, P, WPE, FX, WL, WU, CH>},                    \
+    {k_valu<D, H1, H2, true, false, RW, ROWS, P, WPE, FX, WL, WU, CH>,                     \
+     k_valu<D, H1, H2, true, true, RW, ROWS, P, WPE, FX, WL, WU, CH>}},                    \
+   RW, ROWS, P, WL}
+#define CNF_VARIANT_U(D, H1, H2, RW, ROWS, P, WPE, FX, WL, WU) \
+  CNF_VARIANT_X(D, H1, H2, RW, ROWS, P, WPE, FX, WL, WU, false)
+#define CNF_VARIANT(D, H1, H2, RW, ROWS, P, WPE, FX, WL) \
+  CNF_VARIANT_U(D, H1, H2, RW, ROWS, P, WPE, FX, WL, false)
+
+struct Entry {
+  int D, H1, H2;
+  Variant small, large;  // dispatch on batch size (kLargeBatch)
+  int nf;  // compact floats per net, must equal Shape::valu_net_floats
+};
+
+// Measured on MI355X (tools/bench_variants.py, tools/bench_scaling.py): up to
+// a few M vectors the launch is latency-bound (few waves per SIMD for the
+// whole kernel), where 2 vectors per lane with the weights staged once per
+// block in LDS is fastest; past that the scalar-operand variant with one
+// vector per lane sustains the higher rate.
+constexpr int64_t kLargeBatch = 4ll << 20;
+
+// Shipped configuration per shape: one vector per lane, 256-row tiles.
+#define CNF_VALU(D, H1, H2)                                                     \
+  {D, H1, H2, CNF_VARIANT(D, H1, H2, 2, 256, false, 4, true, true),             \
+   CNF_VARIANT(D, H1, H2, 1, 256, false, 6, true, false), Net<D, H1, H2>::floats}
 
 const Entry kTable[] = {
     // reference default conditioner hidden_size=[5,5] (flows/flows.py:71)
@@ -286,6 +364,40 @@ const Entry kTable[] = {
     CNF_VALU(3, 0, 0), CNF_VALU(10, 0, 0),
     CNF_VALU(10, 7, 0), CNF_VALU(10, 5, 0), CNF_VALU(3, 5, 0),
 };
+
+// A/B variants of the headline shape (CNF_VALU_VARIANT=i, D=10, hidden=[5,5]):
+// rows per lane, threads per block, persistent grid, waves-per-SIMD bound.
+const Variant kExp[] = {
+    CNF_VARIANT(10, 5, 5, 1, 256, false, 6, false, false),                // 0: libm exp
+    CNF_VARIANT(10, 5, 5, 1, 256, false, 6, true, false),                 // 1: = large
+    CNF_VARIANT(10, 5, 5, 2, 256, false, 4, true, true),                  // 2: = small
+    CNF_VARIANT_X(10, 5, 5, 2, 256, false, 4, true, false, false, true),  // 3: chunked, 2/lane
+    CNF_VARIANT(10, 5, 5, 4, 256, false, 2, true, true),                  // 4: LDS, 4/lane
+};
+
+int cu_count() {
+  static int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 256;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return v > 0 ? v : 256;
+  }();
+  return n;
+}
+
+int resident_blocks(KFn fn, int threads) {
+  static std::mutex mu;
+  static std::unordered_map<const void*, int> cache;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = cache.find((const void*)fn);
+  if (it != cache.end()) return it->second;
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, threads, 0) != hipSuccess || n < 1)
+    n = 1;
+  cache[(const void*)fn] = n;
+  return n;
+}
 
 }  // namespace
 
@@ -303,6 +415,15 @@ int valu_run(const Shape& s, const void* prepared, const float* in, float* out, 
   if (s.valu_id < 0) return CNF_ERR_UNSUPPORTED;
   if (B == 0) return CNF_OK;
   const Entry& e = kTable[s.valu_id];
+  if (e.nf != s.valu_net_floats) return CNF_ERR_DESC;  // host/device layout disagree
+  const bool lds_fits =
+      (size_t)256 * 2 * s.D * 4 + (size_t)s.L * s.nets * s.valu_net_floats * 4 <= 64 * 1024;
+  const Variant* var = (B > kLargeBatch || !lds_fits) ? &e.large : &e.small;
+  const char* xv = std::getenv("CNF_VALU_VARIANT");
+  if (xv && e.D == 10 && e.H1 == 5 && e.H2 == 5) {
+    const int k = std::atoi(xv);
+    if (k >= 0 && k < (int)(sizeof(kExp) / sizeof(kExp[0]))) var = &kExp[k];
+  }
   const char* base = static_cast<const char*>(prepared);
   const int32_t* fwd_q = reinterpret_cast<const int32_t*>(base);
   const int32_t* inv_q = fwd_q + s.L * s.D;
@@ -310,8 +431,17 @@ int valu_run(const Shape& s, const void* prepared, const float* in, float* out, 
   const float* W = reinterpret_cast<const float*>(base + idx_bytes(s));
   auto al = [](const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   int vec = al(in) && al(out) && al(all);
-  dim3 grid((unsigned)((B + kRows - 1) / kRows)), block(kRows);
-  hipLaunchKernelGGL(e.fn[inverse ? 1 : 0][s.strict ? 1 : 0], grid, block, 0, st, W,
+  KFn fn = var->fn[inverse ? 1 : 0][s.strict ? 1 : 0];
+  const int64_t tr = (int64_t)var->rows * var->rw;
+  int64_t nblk = (B + tr - 1) / tr;
+  if (var->persist) {
+    const int64_t cap = (int64_t)cu_count() * resident_blocks(fn, var->rows);
+    if (nblk > cap) nblk = cap;
+  }
+  size_t lds = (size_t)tr * s.D * 4;
+  if (var->wl) lds += (size_t)s.L * s.nets * s.valu_net_floats * 4;
+  if (lds > 160 * 1024) return CNF_ERR_UNSUPPORTED;
+  hipLaunchKernelGGL(fn, dim3((unsigned)nblk), dim3(var->rows), lds, st, W,
                      inverse ? inv_q : fwd_q, flags, in, out, ld, all, B, s.L, s.scale, s.shift,
                      s.any_perm ? 1 : 0, vec);
   hipError_t err = hipGetLastError();

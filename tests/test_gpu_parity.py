@@ -54,7 +54,8 @@ def test_forward_matches_reference_fixture(name):
     assert rel_err(ld.cpu().numpy(), d["ld"]) <= TOL
     with torch.no_grad():
         z, ld2 = flow.transform(x)
-    assert torch.equal(z, zs[-1]) and torch.equal(ld2, ld)
+    torch.testing.assert_close(z, zs[-1], rtol=0, atol=0, equal_nan=True)
+    torch.testing.assert_close(ld2, ld, rtol=0, atol=0, equal_nan=True)
 
 
 @pytest.mark.parametrize("name", [n for n in CASES if n != "g6_d4_nan"])
@@ -71,8 +72,20 @@ def test_inverse_matches_reference_fixture(name):
     got = torch.stack(xs).cpu().numpy()
     if d["inv_xs"].shape[0] == 1:
         got = got[-1:]
-    assert rel_err(got, d["inv_xs"]) <= TOL
-    assert rel_err(ld.cpu().numpy(), d["inv_ld"]) <= TOL
+    tol = max(TOL, 2 * _fp32_floor(meta, state, d))
+    assert rel_err(got, d["inv_xs"]) <= tol
+    assert rel_err(ld.cpu().numpy(), d["inv_ld"]) <= tol
+
+
+def _fp32_floor(meta, state, d):
+    """The reference's own fp32-vs-fp64 error on this inverse (numpy oracle in
+    fp64).  Ill-conditioned cases (exp(-s) up to e^7, g6_d10_h0) sit at ~1e-5
+    by themselves; the bar is then twice the reference's own error."""
+    ly = O.cast_layers(O.layers_from_state(state, meta["L"], meta["D"],
+                                           len(meta["hidden"]) + 1, meta["scale"],
+                                           meta["shift"]), np.float64)
+    xs64, _ = O.flow_inverse(ly, d["zs"][-1].astype(np.float64))
+    return rel_err(d["inv_xs"][-1], xs64[-1])
 
 
 def test_fast_mode_on_overflow_case_differs_only_at_reference_nans():
