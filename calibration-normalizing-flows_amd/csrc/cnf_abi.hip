@@ -168,6 +168,18 @@ int cnf_vjp_workspace_bytes(const cnf_desc* desc, int64_t B, size_t* bytes) {
   return vjp_workspace(s, B, bytes);
 }
 
+int cnf_vjp(const cnf_desc* desc, const void* prepared, const float* x, const float* gz,
+            const float* gz_all, const float* gld, float* grads, float* dx, int64_t B,
+            void* workspace, size_t workspace_bytes, void* stream) {
+  Shape s;
+  int st = derive_shape(desc, &s);
+  if (st != CNF_OK) return st;
+  if (B < 0) return CNF_ERR_BATCH;
+  if (!prepared || !grads || (B > 0 && !x)) return CNF_ERR_NULL;
+  return vjp_run(s, prepared, x, nullptr, gz, gz_all, gld, -1, 0.f, 1.f, nullptr, grads, dx, B,
+                 workspace, workspace_bytes, (hipStream_t)stream);
+}
+
 int cnf_loss_vjp(const cnf_desc* desc, const void* prepared, const float* x, const int64_t* y,
                  int32_t loss_kind, float det, float grad_scale, float* loss_terms, float* grads,
                  float* dx, int64_t B, void* workspace, size_t workspace_bytes, void* stream) {
@@ -177,8 +189,8 @@ int cnf_loss_vjp(const cnf_desc* desc, const void* prepared, const float* x, con
   if (B < 0) return CNF_ERR_BATCH;
   if (loss_kind != CNF_LOSS_CAL && loss_kind != CNF_LOSS_CE) return CNF_ERR_DESC;
   if (!prepared || !loss_terms || !grads || (B > 0 && (!x || !y))) return CNF_ERR_NULL;
-  return vjp_run(s, prepared, x, y, loss_kind, det, grad_scale, loss_terms, grads, dx, B,
-                 workspace, workspace_bytes, (hipStream_t)stream);
+  return vjp_run(s, prepared, x, y, nullptr, nullptr, nullptr, loss_kind, det, grad_scale,
+                 loss_terms, grads, dx, B, workspace, workspace_bytes, (hipStream_t)stream);
 }
 
 const char* cnf_kernel_name(const cnf_desc* desc) {

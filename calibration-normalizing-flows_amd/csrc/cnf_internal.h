@@ -68,8 +68,10 @@ int tile_run(const Shape& s, const void* prepared, const float* in, float* out, 
 int prepare_run(const Shape& s, const float* const* params, void* prepared, hipStream_t st);
 
 int vjp_workspace(const Shape& s, int64_t B, size_t* bytes);
-int vjp_run(const Shape& s, const void* prepared, const float* x, const int64_t* y, int kind,
-            float det, float grad_scale, float* loss_terms, float* grads, float* dx, int64_t B,
-            void* ws, size_t ws_bytes, hipStream_t st);
+// kind < 0: generic VJP from gz / gz_all / gld;  kind = CNF_LOSS_*: fused loss
+int vjp_run(const Shape& s, const void* prepared, const float* x, const int64_t* y,
+            const float* gz, const float* gz_all, const float* gld, int kind, float det,
+            float grad_scale, float* loss_terms, float* grads, float* dx, int64_t B, void* ws,
+            size_t ws_bytes, hipStream_t st);
 
 }  // namespace cnf

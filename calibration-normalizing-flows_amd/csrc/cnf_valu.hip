@@ -36,71 +36,6 @@ namespace {
 using namespace valu;
 
 
-// One coupling layer, input in orientation O, output in orientation !O.
-template <int D, int H1, int H2, bool INV, bool STRICT, bool O, bool FX, bool CH, class T>
-__device__ __forceinline__ void step(T* v, T& ld, const float* __restrict__ wl, int scale,
-                                     int shift, int net_floats, bool perm,
-                                     const int32_t* __restrict__ q) {
-  constexpr int DT = D / 2, DC = D - D / 2;
-  constexpr int NO = STRICT ? D : DT;
-  const T zero = splat(0.f, T{});
-  // Inverse: flip (+rev_perm) BEFORE the coupling (flows/flows.py:115-117).
-  constexpr bool OC = INV ? !O : O;  // orientation the coupling sees
-  if constexpr (INV) {
-    if (perm) permute<D, O>(v, q);
-  }
-  T c[DC];
-#pragma unroll
-  for (int k = 0; k < DC; ++k) c[k] = v[R<D, OC>(DT + k)];
-  T p0 = zero;
-  if constexpr (STRICT) {
-    // x_b = mask*x: a non-finite transformed input makes 0*x = NaN feed both nets.
-#pragma unroll
-    for (int j = 0; j < DT; ++j) p0 += 0.f * v[R<D, OC>(j)];
-  }
-  T s[NO], t[NO];
-  if (scale) {
-    mlp<D, H1, H2, NO, STRICT, CH>(wl, c, p0, s);
-    wl += net_floats;
-  } else {
-#pragma unroll
-    for (int j = 0; j < NO; ++j) s[j] = zero;
-  }
-  if (shift) {
-    mlp<D, H1, H2, NO, STRICT, CH>(wl, c, p0, t);
-  } else {
-#pragma unroll
-    for (int j = 0; j < NO; ++j) t[j] = zero;
-  }
-#pragma unroll
-  for (int j = 0; j < DT; ++j) {
-    T& x = v[R<D, OC>(j)];
-    if constexpr (!INV) {
-      T y = fmaV(x, expT<FX>(s[j]), t[j]);
-      x = STRICT ? 0.f * x + y : y;
-      ld += s[j];
-    } else {
-      T y = (x - t[j]) * expT<FX>(-s[j]);
-      x = STRICT ? 0.f * x + y : y;
-      ld -= s[j];
-    }
-  }
-  if constexpr (STRICT) {
-    // masked positions: x + 0*(x*exp(s)+t) is NaN when exp(s) overflows.
-#pragma unroll
-    for (int j = DT; j < D; ++j) {
-      T& x = v[R<D, OC>(j)];
-      T y = INV ? (x - t[j]) * expT<false>(-s[j]) : fmaV(x, expT<false>(s[j]), t[j]);
-      x = x + 0.f * y;
-      ld += 0.f * s[j];
-    }
-  }
-  // Forward: flip (+perm) AFTER the coupling (flows/flows.py:110-112).
-  if constexpr (!INV) {
-    if (perm) permute<D, O>(v, q);
-  }
-}
-
 // Block barrier for LDS hand-offs only: waits for this wave's LDS traffic,
 // not for its outstanding global loads/stores (a __syncthreads() would also
 // drain vmcnt, serialising the prefetch and the output stores).

@@ -102,8 +102,21 @@ int cnf_inverse(const cnf_desc* desc, const void* prepared, const float* z, floa
 #define CNF_LOSS_CAL 0  /* -mean(log(softmax(z_L)[y] + 1e-7) + ld)   calibrators.py:287-291 */
 #define CNF_LOSS_CE 1   /* CE(z_L, y) - det * mean(ld)               run_experiment3D.py:107 */
 
-/* Workspace bytes cnf_loss_vjp needs for a batch of B rows. */
+/* Workspace bytes cnf_vjp / cnf_loss_vjp need for a batch of B rows. */
 int cnf_vjp_workspace_bytes(const cnf_desc* desc, int64_t B, size_t* bytes);
+
+/* Reverse mode of cnf_forward (the autograd backward of Flow.forward):
+ * given upstream gradients of its outputs, writes
+ *   grads  [cnf_param_count]  d/d(parameters), state_dict order (overwritten)
+ *   dx     [B][D]             d/dx, may be NULL
+ * Upstream inputs, each may be NULL (= zero):
+ *   gz     [B][D]     gradient of the final z
+ *   gz_all [L][B][D]  gradient of every layer output (the zs list)
+ *   gld    [B]        gradient of the per-sample log-det
+ * The forward pass is recomputed inside (nothing is saved between calls). */
+int cnf_vjp(const cnf_desc* desc, const void* prepared, const float* x, const float* gz,
+            const float* gz_all, const float* gld, float* grads, float* dx, int64_t B,
+            void* workspace, size_t workspace_bytes, void* stream);
 
 /* Fused forward + loss + reverse mode.  Writes
  *   loss_terms[3]   {sum over rows of the per-row loss, sum of ce, sum of ld}

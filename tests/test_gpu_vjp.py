@@ -1,0 +1,133 @@
+"""Reverse mode (cnf_vjp / cnf_loss_vjp) against the reference's own autograd
+gradients (golden g5 fixtures) and the numpy oracle's hand-written backward."""
+import numpy as np
+import pytest
+import torch
+
+from _golden import load, names
+from _model import build_flow
+from cnf_hip import engine
+from cnf_hip import vjp as V
+from oracle import cnf_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _grad_err(got, ref):
+    sc = float(np.max(np.abs(ref))) + 1e-3
+    return float(np.max(np.abs(got - ref))) / sc
+
+
+@pytest.mark.parametrize("name", [n for n in names("g5") if "d100" not in n])
+@pytest.mark.parametrize("kind", ["cal", "ce"])
+def test_fused_loss_grads_match_reference_autograd(name, kind):
+    meta, state, d = load(name)
+    flow = build_flow(meta, state, DEV)
+    stack = flow._native_stack()
+    x = torch.from_numpy(d["x"]).to(DEV)
+    y = torch.from_numpy(d["y"]).to(DEV)
+    B = x.shape[0]
+    terms, grads, _ = V.loss_and_grads(stack, x, y, kind=0 if kind == "cal" else 1, det=1.0,
+                                       grad_scale=1.0 / B)
+    terms = terms.cpu().numpy()
+    ref_loss = float(d["loss_" + kind])
+    assert abs(terms[0] / B - ref_loss) / (abs(ref_loss) + 1) <= 1e-5
+    worst = 0.0
+    for (k, p), g in zip([(k, p) for k, p in flow.named_parameters() if p.requires_grad],
+                         V._split(stack, grads)):
+        worst = max(worst, _grad_err(g.cpu().numpy(), d["g%s:%s" % (kind, k)]))
+    assert worst <= 1e-4, worst
+
+
+def test_autograd_backward_matches_reference():
+    meta, state, d = load("g5_grads_d10")
+    flow = build_flow(meta, state, DEV)
+    x = torch.from_numpy(d["x"]).to(DEV)
+    y = torch.from_numpy(d["y"]).to(DEV)
+    n0 = engine.stats["vjp"]
+    zs, ld = flow(x)
+    probs = torch.softmax(zs[-1], dim=1)
+    ce = torch.log(probs.gather(1, y.view(-1, 1)) + 1e-7)
+    loss = -torch.mean(ce.squeeze() + ld)          # calibrators.py:288-291
+    flow.zero_grad()
+    loss.backward()
+    assert engine.stats["vjp"] == n0 + 1, "native cnf_vjp did not run"
+    assert abs(loss.item() - float(d["loss_cal"])) <= 1e-5 * (abs(float(d["loss_cal"])) + 1)
+    worst = 0.0
+    for k, p in flow.named_parameters():
+        if p.requires_grad:
+            worst = max(worst, _grad_err(p.grad.cpu().numpy(), d["gcal:" + k]))
+    assert worst <= 1e-4, worst
+
+
+def _flow(D, L, hidden, sigma, seed, scale=True, shift=True, flip=False):
+    from flows.flows import Flow, NvpCouplingLayer
+    torch.manual_seed(seed)
+    np.random.seed(seed)
+    f = Flow([NvpCouplingLayer(D, hidden, scale=scale, shift=shift, random_flip=flip)
+              for _ in range(L)])
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for p in f.parameters():
+            if p.requires_grad:
+                p.copy_(torch.randn(p.shape, generator=g) * sigma)
+    return f
+
+
+@pytest.mark.parametrize("D,L,hidden,scale,shift,flip", [
+    (10, 6, [5, 5], True, True, False),
+    (10, 5, [5, 5], True, True, True),     # odd L, random_flip
+    (3, 2, [5, 5], False, True, False),    # NICE
+    (10, 3, [5, 5], True, False, False),   # shift=False
+    (10, 3, [], True, True, False),
+    (10, 3, [7], True, True, False),
+])
+def test_vjp_all_outputs_and_dx_against_cpu_autograd(D, L, hidden, scale, shift, flip):
+    f = _flow(D, L, hidden, 0.2, 3, scale, shift, flip)
+    x = torch.randn(777, D, generator=torch.Generator().manual_seed(1))
+    w = torch.randn(L, 777, D, generator=torch.Generator().manual_seed(2))
+    wl = torch.randn(777, generator=torch.Generator().manual_seed(3))
+
+    def objective(flow, xx):
+        zs, ld = flow(xx)
+        return sum((z * w[i].to(z.device)).sum() for i, z in enumerate(zs)) + \
+            (ld * wl.to(ld.device)).sum()
+
+    xc = x.clone().requires_grad_(True)
+    objective(f, xc).backward()
+    ref = {k: p.grad.clone() for k, p in f.named_parameters() if p.requires_grad}
+    fg = f.to(DEV)
+    fg.zero_grad()
+    xg = x.to(DEV).requires_grad_(True)
+    n0 = engine.stats["vjp"]
+    objective(fg, xg).backward()
+    assert engine.stats["vjp"] == n0 + 1
+    for k, p in fg.named_parameters():
+        if p.requires_grad:
+            assert _grad_err(p.grad.cpu().numpy(), ref[k].numpy()) <= 1e-4, k
+    assert _grad_err(xg.grad.cpu().numpy(), xc.grad.numpy()) <= 1e-4
+
+
+def test_vjp_is_deterministic_and_matches_oracle_at_scale():
+    f = _flow(10, 6, [5, 5], 0.1, 4).to(DEV)
+    stack = f._native_stack()
+    B = 1 << 20
+    g = torch.Generator(device=DEV).manual_seed(0)
+    x = torch.randn(B, 10, device=DEV, generator=g)
+    y = torch.randint(0, 10, (B,), device=DEV, generator=g)
+    t1, g1, _ = V.loss_and_grads(stack, x, y, grad_scale=1.0 / B)
+    t2, g2, _ = V.loss_and_grads(stack, x, y, grad_scale=1.0 / B)
+    assert torch.equal(g1, g2) and torch.equal(t1, t2), "non-deterministic reduction"
+    # the mean over 1M rows equals the mean of per-shard means (linearity), and a
+    # 4096-row slice agrees with the numpy oracle
+    st = {k: v.cpu().numpy() for k, v in f.state_dict().items()}
+    ol = O.layers_from_state(st, 6, 10, 3)
+    xs, ys = x[:4096], y[:4096]
+    tl, gl, _ = V.loss_and_grads(stack, xs, ys, grad_scale=1.0 / 4096)
+    loss, og = O.loss_and_grads(ol, xs.cpu().numpy(), ys.cpu().numpy(), "cal")
+    assert abs(tl[0].item() / 4096 - loss) / (abs(loss) + 1) <= 1e-5
+    flat = np.concatenate([np.concatenate([np.concatenate([gw.ravel(), gb.ravel()])
+                                           for gw, gb in og[l][n]])
+                           for l in range(6) for n in ("s", "t")])
+    assert _grad_err(gl.cpu().numpy(), flat) <= 1e-4
