@@ -3,10 +3,13 @@
 Workload (BASELINE.json configs[1]): 6-layer RealNVP affine
 coupling, D=10 logits, conditioner hidden_size=[5,5] (reference default,
 flows/flows.py:71), B=2^20 synthetic logit vectors per GPU, fp32.  One step =
-one fused forward + per-sample log-det pass over one batch (cnf_forward through
-the C ABI: final z [B,10] + log-det [B]).  With N>1 ranks every rank runs its
-own 2^20-vector shard (weak scaling, batch 8M at N=8 = configs[2]) and the step
-ends with the RCCL all-reduce of the shard's NLL sum (configs[2]).
+one fused forward + per-sample log-det pass over one batch that also reduces
+the batch's calibration NLL (cnf_forward_loss through the C ABI: writes the
+final z [B,10] and log-det [B], and the sums of the per-row loss / ce / ld --
+the eval pass of TorchFlowCalibrator.fit, calibrators.py:297-317).  With N>1
+ranks every rank runs its own 2^20-vector shard (weak scaling: 8M vectors at
+N=8 = configs[2]) and the step ends with the RCCL all-reduce of the shard's
+3 NLL sums (configs[2]); at N=1 there is nothing to reduce.
 
 Inputs are resident in HBM before timing; the step rotates through enough
 distinct input/output buffers (>= --rotate-gb) that the 256 MB Infinity Cache
@@ -54,8 +57,9 @@ def algo_flops_per_vec(D, L, hidden, scale=True):
     return L * per_layer
 
 
-def algo_bytes_per_vec(D, L, all_outputs=False):
-    return 4 * D + 4 * D * (L if all_outputs else 1) + 4
+def algo_bytes_per_vec(D, L, all_outputs=False, labels=False):
+    """x in, z out (every layer's z with all_outputs), log-det out, int64 label in."""
+    return 4 * D + 4 * D * (L if all_outputs else 1) + 4 + (8 if labels else 0)
 
 
 def make_flow(w, device, seed=0):
@@ -81,9 +85,10 @@ def synthetic_logits(B, D, device, seed):
 
 
 class Runner:
-    """Pre-built C-ABI launches of one fused pass over rotating buffers."""
+    """Pre-built C-ABI launches of one fused pass over rotating buffers.
+    mode: "forward" (cnf_forward / cnf_inverse), "loss" (cnf_forward_loss)."""
 
-    def __init__(self, w, device, rotate_bytes, all_outputs=False):
+    def __init__(self, w, device, rotate_bytes, all_outputs=False, mode="forward"):
         from cnf_hip import _lib
         self.w = w
         self.dev = device
@@ -92,7 +97,8 @@ class Runner:
         self.blob = self.stack.prepared(device)
         self.lib = _lib.lib()
         B, D, L = w["B"], w["D"], w["L"]
-        per_set = algo_bytes_per_vec(D, L, all_outputs) * B
+        self.mode = mode
+        per_set = algo_bytes_per_vec(D, L, all_outputs, mode == "loss") * B
         self.nsets = max(1, min(64, math.ceil(rotate_bytes / per_set)))
         self.sets = []
         for i in range(self.nsets):
@@ -108,14 +114,34 @@ class Runner:
         P = ctypes.c_void_p
         vp = lambda t: P(t.data_ptr()) if t is not None else P(0)
         self.stream = torch.cuda.current_stream(device)
-        self.args = [(vp(x), vp(out), vp(ld), vp(allt)) for (x, y, out, ld, allt) in self.sets]
+        self.args = [(vp(x), vp(out), vp(ld), vp(allt), vp(y)) for (x, y, out, ld, allt) in
+                     self.sets]
+        self.terms = torch.zeros(3, device=device)
+        if mode == "loss":
+            n = ctypes.c_size_t()
+            st = self.lib.cnf_forward_loss_workspace_bytes(self.desc, ctypes.c_int64(B),
+                                                           ctypes.byref(n))
+            if st != 0:
+                raise RuntimeError("cnf_forward_loss unsupported for this shape: %d" % st)
+            self.ws = torch.empty(max(n.value, 16), dtype=torch.uint8, device=device)
+            self.ws_bytes = n.value
         self.i = 0
 
     def step(self):
         a = self.args[self.i % self.nsets]
         self.i += 1
-        st = self.fn(self.desc, ctypes.c_void_p(self.blob.data_ptr()), a[0], a[1], a[2], a[3],
-                     ctypes.c_int64(self.w["B"]), ctypes.c_void_p(self.stream.cuda_stream))
+        blob = ctypes.c_void_p(self.blob.data_ptr())
+        stream = ctypes.c_void_p(self.stream.cuda_stream)
+        if self.mode == "loss":
+            st = self.lib.cnf_forward_loss(self.desc, blob, a[0], a[4], ctypes.c_int32(0),
+                                           ctypes.c_float(1.0), a[1], a[2],
+                                           ctypes.c_void_p(self.terms.data_ptr()),
+                                           ctypes.c_int64(self.w["B"]),
+                                           ctypes.c_void_p(self.ws.data_ptr()),
+                                           ctypes.c_size_t(self.ws_bytes), stream)
+        else:
+            st = self.fn(self.desc, blob, a[0], a[1], a[2], a[3], ctypes.c_int64(self.w["B"]),
+                         stream)
         if st != 0:
             raise RuntimeError("cnf launch failed: %d" % st)
 
@@ -150,6 +176,28 @@ def kernel_only_seconds(runner, launches):
     (HIP events on the launch stream, no collective in between)."""
     t, _ = runner.timed(launches, 3)
     return t / launches
+
+
+def train_step_rate(dev, B=1 << 20, steps=20):
+    """Fused calibrator training step (cnf_loss_vjp: forward + loss + reverse
+    mode + fixed-order gradient reduction) on the cfg2 shape: vectors/s."""
+    from cnf_hip import vjp as V
+    w = WORKLOADS["cfg2"]
+    flow = make_flow(w, dev)
+    stack = flow._native_stack()
+    x, y = synthetic_logits(B, w["D"], dev, 4321)
+    for _ in range(3):
+        V.loss_and_grads(stack, x, y, grad_scale=1.0 / B)
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(steps):
+        V.loss_and_grads(stack, x, y, grad_scale=1.0 / B)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    t = e0.elapsed_time(e1) / 1e3 / steps
+    return {"vec_per_s": round(B / t, 1), "ms_per_step": round(t * 1e3, 4), "B": B,
+            "note": "forward + calibrator loss + VJP + gradient reduction; optimizer excluded"}
 
 
 def cpu_baseline(w, seconds=10.0):
@@ -200,20 +248,15 @@ def main():
     w = dict(WORKLOADS[args.workload])
     if args.batch:
         w["B"] = args.batch
-    runner = Runner(w, dev, args.rotate_gb * 1e9)
+    mode = "loss" if (w["D"] <= 16 and not w["inverse"]) else "forward"
+    runner = Runner(w, dev, args.rotate_gb * 1e9, mode=mode)
 
     collective = None
     if world > 1:
-        # NLL all-reduce over xGMI (configs[2]): each rank reduces its shard's
-        # per-row log-det sum; one 2-float RCCL all-reduce per step.
-        red = torch.zeros(2, device=dev)
-
+        # NLL all-reduce over xGMI (configs[2]): the shard's (loss, ce, ld) sums,
+        # written by the fused kernel, summed across ranks by one RCCL call.
         def collective():
-            ld = runner.sets[(runner.i - 1) % runner.nsets][3]
-            red[0] = ld.sum()
-            red[1] = float(w["B"])
-            dist.all_reduce(red)
-        collective = collective
+            dist.all_reduce(runner.terms)
 
     t_dev, wall = runner.timed(args.steps, args.warmup, collective)
     t = torch.tensor([t_dev], dtype=torch.float64, device=dev)
@@ -225,7 +268,7 @@ def main():
 
     # dominant kernel: average device time per launch, no collective in between
     k_avg = kernel_only_seconds(runner, max(50, args.steps // 2))
-    bytes_vec = algo_bytes_per_vec(w["D"], w["L"])
+    bytes_vec = algo_bytes_per_vec(w["D"], w["L"], labels=(mode == "loss"))
     flops_vec = algo_flops_per_vec(w["D"], w["L"], w["hidden"], w["scale"])
     achieved_gbs = w["B"] * bytes_vec / k_avg / 1e9
     achieved_tf = w["B"] * flops_vec / k_avg / 1e12
@@ -238,6 +281,8 @@ def main():
         "frac": None, "traffic": None,
         "kernel": runner.stack.kernel_name(),
         "kernel_avg_us": round(k_avg * 1e6, 3),
+        "timed_kernels": "k_valu (fused pass) + k_reduce (fixed-order NLL sum)" if mode == "loss"
+                         else "k_valu",
         "algo_bytes_per_vec": bytes_vec, "algo_flops_per_vec": flops_vec,
         "valu_tflops": round(achieved_tf, 2), "valu_frac": round(achieved_tf / VALU_PEAK_TFLOPS, 4),
         "rotating_sets": runner.nsets,
@@ -246,9 +291,11 @@ def main():
 
     variants = {}
     if rank == 0 and world == 1 and not args.no_variants:
-        for name, wl, allo in (("cfg2_all_zs", WORKLOADS["cfg2"], True),
+        for name, wl, allo in (("cfg2_forward_ld", WORKLOADS["cfg2"], False),
+                               ("cfg2_all_zs", WORKLOADS["cfg2"], True),
                                ("cfg5_inverse", WORKLOADS["cfg5"], False),
-                               ("cfg4_d100", WORKLOADS["cfg4"], False)):
+                               ("cfg4_d100", WORKLOADS["cfg4"], False),
+                               ("cfg1_nice_d3", WORKLOADS["cfg1"], False)):
             r = Runner(dict(wl), dev, args.rotate_gb * 1e9, all_outputs=allo)
             ka = kernel_only_seconds(r, 30)
             bv = algo_bytes_per_vec(wl["D"], wl["L"], allo)
@@ -259,6 +306,7 @@ def main():
                               "tflops": round(wl["B"] * fv / ka / 1e12, 2)}
             del r
             torch.cuda.empty_cache()
+        variants["cfg2_train_step_fused_loss_vjp"] = train_step_rate(dev)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -282,6 +330,9 @@ def main():
                        "global_batch": w["B"] * world, "parallelism": "dp%d" % world,
                        "hidden_size": w["hidden"], "weights": "N(0,0.1) synthetic"},
             "roofline": roof,
+        "step": "fused forward + log-det + NLL sums (cnf_forward_loss)%s" % (
+            " + RCCL all-reduce of the NLL sums" if world > 1 else "") if mode == "loss"
+            else "fused pass (cnf_%s)" % ("inverse" if w["inverse"] else "forward"),
             "cpu_baseline": cpu,
             "wall_s": round(wall, 4),
         }

@@ -1,0 +1,223 @@
+"""Drop-in mirror of the reference's calibrators.py for the flow calibrator.
+
+`Calibrator` (base: logit centring, one-hot targets, prior correction) and
+`TorchFlowCalibrator` keep the reference's constructor, `fit` schedule, history
+format and `predict` path (calibrators.py:13-44, 239-353).  When the flow built
+by the factory is a stack of NvpCouplingLayers on a ROCm device, each training
+step is ONE fused native launch (forward + calibrator loss + reverse mode,
+cnf_loss_vjp) followed by the optimizer step, and the per-epoch evaluation is
+ONE fused forward + loss launch (cnf_forward_loss); history entries stay
+device tensors, as in the reference, so no step synchronises the host.
+Any other flow (or a CPU device) runs the reference's own torch loop.
+
+Out of scope here (host-side, non-flow calibrators of the reference):
+TempScaling / Matrix / Vector / MLR / PAV calibrators (calibrators.py:55-236).
+"""
+import numpy as np
+import torch
+from scipy.special import softmax
+from torch import nn
+from torch.utils.data import DataLoader, TensorDataset
+
+
+def _onehot(target, n_classes=None):
+    """utils/ops.py:42-51 (onehot_encode)."""
+    target = np.asarray(target).astype(int).reshape(-1)
+    n = int(target.max()) + 1 if n_classes is None else n_classes
+    out = np.zeros((target.shape[0], n))
+    out[np.arange(target.shape[0]), target] = 1
+    return out
+
+
+class Calibrator:
+    """Abstract calibrator (calibrators.py:13-44)."""
+
+    def __init__(self, logits, target):
+        logits = logits - np.mean(logits, axis=1, keepdims=True)
+        self.logits = logits
+        if target.shape != logits.shape:
+            target = _onehot(target, logits.shape[1])
+        self.target = target
+        (_, self.n_classes) = target.shape
+        self.log_priors = self._get_log_priors(target)
+
+    def __call__(self, logits):
+        return self.predict(logits)
+
+    def _get_log_priors(self, target):
+        priors = np.sum(target, axis=0)
+        priors = priors / np.sum(priors)
+        return np.log(priors)
+
+    def predict_post(self, logits):
+        raise NotImplementedError
+
+    def predict(self, logits):
+        logits = logits - np.mean(logits, axis=1, keepdims=True)
+        probs = self.predict_post(logits)
+        return softmax(np.log(probs + 1e-7) - self.log_priors, axis=1)
+
+
+class DummyCalibrator(Calibrator):
+    """Uncalibrated model (calibrators.py:47-53)."""
+
+    def predict_post(self, logits):
+        return softmax(logits, axis=1)
+
+
+def _native_stack(flow, dev):
+    """The fused CouplingStack behind `flow`, or None when the flow is not a
+    stack of NvpCouplingLayers or the device is not a ROCm GPU."""
+    if torch.device(dev).type != "cuda":
+        return None
+    try:
+        from flows.flows import Flow, NvpCouplingLayer
+        from cnf_hip import _lib
+    except ImportError:
+        return None
+    if not isinstance(flow, Flow) or not all(isinstance(l, NvpCouplingLayer) for l in flow.layers):
+        return None
+    if flow._strict():
+        return None
+    stack = flow._native_stack()
+    try:
+        import ctypes
+        n = ctypes.c_size_t()
+        st = _lib.lib().cnf_vjp_workspace_bytes(ctypes.byref(stack.desc), ctypes.c_int64(1),
+                                                ctypes.byref(n))
+    except Exception:
+        return None
+    return stack if st == 0 else None
+
+
+class TorchFlowCalibrator(Calibrator):
+    """Trains a normalizing flow on (logits, target) by minimising
+    -mean(log(softmax(f(x))[y] + 1e-7) + log|det J_f(x)|)  (calibrators.py:239-353)."""
+
+    def __init__(self, Flow, logits, target, **kwargs):
+        super().__init__(logits, target)
+        self.target = np.argmax(self.target, axis=1)
+        self.logits = torch.as_tensor(self.logits, dtype=torch.float)
+        self.target = torch.as_tensor(self.target, dtype=torch.long)
+        self.flow = Flow(self.n_classes, **kwargs)
+        self.dev = kwargs.get('dev', torch.device("cuda") if torch.cuda.is_available()
+                              else torch.device("cpu"))
+        self.CE = nn.CrossEntropyLoss()
+        self.optimizer = torch.optim.Adam(self.flow.parameters())
+        self._replica = None
+        self.history = self.fit(self.logits, self.target,
+                                epochs=kwargs.get('epochs', 1000),
+                                batch_size=kwargs.get('batch_size', logits.shape[0]))
+
+    # ------------------------------------------------------------------ fit
+    def fit(self, logits, target, epochs, batch_size):
+        logits = logits.to(self.dev)
+        target = target.to(self.dev)
+        self.flow.to(self.dev)
+        stack = _native_stack(self.flow, self.dev)
+        if stack is not None:
+            history = self._fit_native(stack, logits, target, epochs, batch_size)
+        else:
+            history = self._fit_torch(logits, target, epochs, batch_size)
+        self.flow.cpu()
+        if torch.cuda.is_available():
+            torch.cuda.empty_cache()
+        return history
+
+    def _fit_torch(self, logits, target, epochs, batch_size):
+        """The reference's loop (calibrators.py:273-317), unchanged semantics."""
+        train_dl = DataLoader(TensorDataset(logits, target), batch_size=batch_size, shuffle=True)
+        history = {'loss': [], 'ce': [], 'log_det': []}
+        softmx = nn.Softmax(dim=1)
+        for epoch in range(epochs):
+            self.flow.train()
+            for xb, yb in train_dl:
+                pred, log_det = self.flow(xb)
+                probs = softmx(pred)
+                ce = torch.log(probs.gather(1, yb.view(-1, 1)) + 1e-7)
+                loss = -torch.mean(ce.squeeze() + log_det)
+                self.flow.zero_grad()
+                loss.backward()
+                self.optimizer.step()
+            self.flow.eval()
+            _loss = _ce = _log_det = 0
+            num = 0
+            with torch.no_grad():
+                for xb, yb in train_dl:
+                    pred, log_det = self.flow(xb)
+                    probs = softmx(pred)
+                    ce = torch.log(probs.gather(1, yb.view(-1, 1)) + 1e-7)
+                    log_prob = ce.squeeze() + log_det
+                    # the reference ASSIGNS per batch (calibrators.py:308-313): the
+                    # history keeps the last batch's sums over the total count
+                    _loss = -torch.mean(log_prob) * len(xb)
+                    _ce = -torch.mean(ce.squeeze()) * len(xb)
+                    _log_det = torch.mean(log_det) * len(xb)
+                    num += len(xb)
+                history['loss'].append(_loss / num)
+                history['ce'].append(_ce / num)
+                history['log_det'].append(_log_det / num)
+        return history
+
+    def _fit_native(self, stack, logits, target, epochs, batch_size):
+        """Same schedule on the fused kernels: one cnf_loss_vjp launch per
+        training batch, one cnf_forward_loss launch per evaluation batch."""
+        from cnf_hip import vjp as V
+        params = stack.param_tensors()
+        N = logits.shape[0]
+        history = {'loss': [], 'ce': [], 'log_det': []}
+        gen = torch.Generator(device=logits.device)
+        gen.manual_seed(int(torch.randint(0, 2 ** 62, (1,)).item()))
+        for epoch in range(epochs):
+            self.flow.train()
+            order = torch.randperm(N, device=logits.device, generator=gen)  # shuffle=True
+            for s in range(0, N, batch_size):
+                idx = order[s:s + batch_size]
+                xb, yb = logits.index_select(0, idx), target.index_select(0, idx)
+                _, grads, _ = V.loss_and_grads(stack, xb, yb, grad_scale=1.0 / xb.shape[0])
+                for p, g in zip(params, V._split(stack, grads)):
+                    p.grad = g
+                self.optimizer.step()
+            self.flow.eval()
+            order = torch.randperm(N, device=logits.device, generator=gen)
+            num = 0
+            terms = None
+            for s in range(0, N, batch_size):
+                idx = order[s:s + batch_size]
+                terms, _, _ = stack.forward_loss(logits.index_select(0, idx),
+                                                 target.index_select(0, idx))
+                num += idx.numel()
+            history['loss'].append(terms[0] / num)
+            history['ce'].append(terms[1] / num)
+            history['log_det'].append(terms[2] / num)
+        for p in params:
+            p.grad = None
+        return history
+
+    # -------------------------------------------------------------- predict
+    def _device_flow(self):
+        """A device-resident replica of the (CPU) flow, refreshed only when a
+        parameter changed -- the reference moves the flow to the device and
+        back on every call (calibrators.py:335-343)."""
+        import copy
+        key = tuple((p.data_ptr(), p._version) for p in self.flow.parameters())
+        if self._replica is None or self._replica[0] != key:
+            rep = copy.deepcopy(self.flow).to(self.dev)
+            rep.eval()
+            self._replica = (key, rep)
+        return self._replica[1]
+
+    def predict_logits(self, logits):
+        logits = torch.as_tensor(logits, dtype=torch.float)
+        if torch.device(self.dev).type == "cuda":
+            flow = self._device_flow()
+            with torch.no_grad():
+                preds, _ = flow(logits.to(self.dev))
+            return preds.cpu().numpy()
+        self.flow.to(self.dev)
+        preds, _ = self.flow(logits.to(self.dev))
+        return preds.cpu().detach().numpy()
+
+    def predict_post(self, logits):
+        logits = self.predict_logits(logits)
+        return softmax(logits, axis=1)

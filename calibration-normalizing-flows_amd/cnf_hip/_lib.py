@@ -24,7 +24,8 @@ LOSS_CE = 1
 # Every symbol include/cnf.h declares (checked by tests/test_abi.py).
 EXPORTS = (
     "cnf_param_count", "cnf_param_tensor_count", "cnf_prepared_bytes", "cnf_prepare",
-    "cnf_forward", "cnf_inverse", "cnf_vjp_workspace_bytes", "cnf_vjp", "cnf_loss_vjp",
+    "cnf_forward", "cnf_inverse", "cnf_forward_loss_workspace_bytes", "cnf_forward_loss",
+    "cnf_vjp_workspace_bytes", "cnf_vjp", "cnf_loss_vjp",
     "cnf_kernel_name", "cnf_strerror", "cnf_last_hip_error", "cnf_abi_version",
 )
 
@@ -72,6 +73,10 @@ def _bind(lib):
         "cnf_prepare": (ctypes.c_int, [D, ctypes.POINTER(P), P, P]),
         "cnf_forward": (ctypes.c_int, [D, P, P, P, P, P, I64, P]),
         "cnf_inverse": (ctypes.c_int, [D, P, P, P, P, P, I64, P]),
+        "cnf_forward_loss_workspace_bytes": (ctypes.c_int,
+                                             [D, I64, ctypes.POINTER(ctypes.c_size_t)]),
+        "cnf_forward_loss": (ctypes.c_int, [D, P, P, P, I32, F, P, P, P, I64, P, ctypes.c_size_t,
+                                            P]),
         "cnf_vjp_workspace_bytes": (ctypes.c_int, [D, I64, ctypes.POINTER(ctypes.c_size_t)]),
         "cnf_vjp": (ctypes.c_int, [D, P, P, P, P, P, P, P, I64, P, ctypes.c_size_t, P]),
         "cnf_loss_vjp": (ctypes.c_int, [D, P, P, P, I32, F, F, P, P, P, I64, P, ctypes.c_size_t,

@@ -50,6 +50,7 @@ class CouplingStack:
         self.desc = _lib.make_desc(self.dim, self.L, self.hidden, self.scale, self.shift,
                                    self.strict_nan, self._perms)
         self._cache = {}
+        self._loss_ws = {}
 
     @staticmethod
     def compatible(layers):
@@ -133,6 +134,34 @@ class CouplingStack:
         if want_all and want_final:
             fin = allt[-1]
         return fin, ld, allt
+
+    def forward_loss(self, x, y, kind=_lib.LOSS_CAL, det=1.0, want_outputs=False):
+        """Fused forward + log-det + loss terms (cnf_forward_loss): returns
+        (terms[3] = sums over the rows of (loss, ce, log-det), z or None, ld or None)."""
+        x = self._check_input(x)
+        y = y.contiguous().to(torch.int64)
+        B = x.shape[0]
+        dev = x.device
+        blob = self.prepared(dev)
+        lib = _lib.lib()
+        n = ctypes.c_size_t()
+        _lib.check("cnf_forward_loss_workspace_bytes",
+                   lib.cnf_forward_loss_workspace_bytes(ctypes.byref(self.desc),
+                                                        ctypes.c_int64(B), ctypes.byref(n)))
+        ws = self._loss_ws.get(dev)
+        if ws is None or ws.numel() < n.value:
+            ws = torch.empty(max(n.value, 16), dtype=torch.uint8, device=dev)
+            self._loss_ws[dev] = ws
+        terms = torch.empty(3, dtype=torch.float32, device=dev)
+        z = torch.empty_like(x) if want_outputs else None
+        ld = torch.empty(B, dtype=torch.float32, device=dev) if want_outputs else None
+        st = lib.cnf_forward_loss(ctypes.byref(self.desc), _ptr(blob), _ptr(x), _ptr(y),
+                                  ctypes.c_int32(kind), ctypes.c_float(det), _ptr(z), _ptr(ld),
+                                  _ptr(terms), ctypes.c_int64(B), _ptr(ws),
+                                  ctypes.c_size_t(n.value), _stream(dev))
+        _lib.check("cnf_forward_loss", st)
+        stats["forward"] += 1
+        return terms, z, ld
 
     # -------------------------------------------------------------- autograd
     def forward_autograd(self, x, want_all):

@@ -159,6 +159,52 @@ int cnf_inverse(const cnf_desc* desc, const void* prepared, const float* z, floa
   return run(desc, prepared, z, x, logdet, x_all, B, stream, true);
 }
 
+int cnf_forward_loss_workspace_bytes(const cnf_desc* desc, int64_t B, size_t* bytes) {
+  Shape s;
+  int st = derive_shape(desc, &s);
+  if (st != CNF_OK) return st;
+  if (!bytes) return CNF_ERR_NULL;
+  if (B < 0) return CNF_ERR_BATCH;
+  if (s.family != Family::kValu) return CNF_ERR_UNSUPPORTED;
+  const int nb = B > 0 ? valu_loss_blocks(s, B) : 0;
+  *bytes = (size_t)(nb > 0 ? nb : 1) * 4 * sizeof(float);
+  return CNF_OK;
+}
+
+int cnf_forward_loss(const cnf_desc* desc, const void* prepared, const float* x,
+                     const int64_t* y, int32_t loss_kind, float det, float* z, float* logdet,
+                     float* loss_terms, int64_t B, void* workspace, size_t workspace_bytes,
+                     void* stream) {
+  Shape s;
+  int st = derive_shape(desc, &s);
+  if (st != CNF_OK) return st;
+  if (B < 0) return CNF_ERR_BATCH;
+  if (loss_kind != CNF_LOSS_CAL && loss_kind != CNF_LOSS_CE) return CNF_ERR_DESC;
+  if (s.family != Family::kValu) return CNF_ERR_UNSUPPORTED;
+  if (!prepared || !loss_terms || (B > 0 && (!x || !y))) return CNF_ERR_NULL;
+  size_t need = 0;
+  st = cnf_forward_loss_workspace_bytes(desc, B, &need);
+  if (st != CNF_OK) return st;
+  if (!workspace || workspace_bytes < need) return CNF_ERR_NULL;
+  auto mis = [](const void* p) { return p && (reinterpret_cast<uintptr_t>(p) & 3); };
+  if (mis(x) || mis(z) || mis(logdet)) return CNF_ERR_ALIGN;
+  float* part = static_cast<float*>(workspace);
+  int nb = 0;
+  if (B > 0) {
+    nb = valu_loss_blocks(s, B);
+    st = valu_run(s, prepared, x, z, logdet, nullptr, B, false, (hipStream_t)stream, y, part,
+                  loss_kind, det);
+    if (st != CNF_OK) return st;
+  }
+  reduce_partials(part, nb, 4, 0, nullptr, loss_terms, (hipStream_t)stream);
+  hipError_t err = hipGetLastError();
+  if (err != hipSuccess) {
+    set_hip_error(err);
+    return CNF_ERR_HIP;
+  }
+  return CNF_OK;
+}
+
 int cnf_vjp_workspace_bytes(const cnf_desc* desc, int64_t B, size_t* bytes) {
   Shape s;
   int st = derive_shape(desc, &s);

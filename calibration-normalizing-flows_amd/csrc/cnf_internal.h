@@ -59,7 +59,12 @@ void set_hip_error(hipError_t e);
 // ---- kernel-family entry points (return cnf_status) ----
 int valu_supported(const Shape& s);  // -> valu_id or -1
 int valu_run(const Shape& s, const void* prepared, const float* in, float* out, float* ld,
-             float* all, int64_t B, bool inverse, hipStream_t st);
+             float* all, int64_t B, bool inverse, hipStream_t st, const int64_t* y = nullptr,
+             float* loss_part = nullptr, int kind = 0, float det = 0.f);
+int valu_loss_blocks(const Shape& s, int64_t B);  // per-block loss partials of the fused eval
+// sum partials[b][i] over b in block order: grads[i] (i < P), terms[i - P] (i < P + 3)
+int reduce_partials(const float* partials, int nblk, int PS, int P, float* grads, float* terms,
+                    hipStream_t st);
 
 int tile_configure(Shape* s);        // fills tile_* fields; CNF_OK or UNSUPPORTED
 int tile_run(const Shape& s, const void* prepared, const float* in, float* out, float* ld,

@@ -109,6 +109,69 @@ __device__ __forceinline__ void store_rows(float* __restrict__ dst, float* sm, c
   tile_store<ROWS>(dst, sm, nrows * D, vec);
 }
 
+__device__ __forceinline__ float comp(float v, int) { return v; }
+template <class V>
+__device__ __forceinline__ float comp(V v, int q) { return v[q]; }
+
+// Per-row terms of the calibrator loss on the final logits z (logical order):
+// CAL: loss = -(log(softmax(z)[y] + 1e-7) + ld)       calibrators.py:288-291
+// CE:  loss = -log_softmax(z)[y] - det * ld            run_experiment3D.py:107
+template <int D>
+__device__ __forceinline__ void row_loss(const float* z, float ld, int y, int kind, float det,
+                                         float& t0, float& t1, float& t2) {
+  float m = z[0];
+#pragma unroll
+  for (int j = 1; j < D; ++j) m = fmaxf(m, z[j]);
+  float se = 0.f, zy = z[0];
+#pragma unroll
+  for (int j = 0; j < D; ++j) {
+    se += expf(z[j] - m);
+    zy = (j == y) ? z[j] : zy;
+  }
+  const float lpy = zy - (m + logf(se));
+  float ce, loss;
+  if (kind == CNF_LOSS_CAL) {
+    ce = -logf(expf(lpy) + 1e-7f);
+    loss = ce - ld;
+  } else {
+    ce = -lpy;
+    loss = ce - det * ld;
+  }
+  t0 += loss;
+  t1 += ce;
+  t2 += ld;
+}
+
+// Block sum of three per-thread values in a fixed order -> dst[0..2].
+template <int ROWS>
+__device__ __forceinline__ void block_sum3(float a, float b, float c, float* sm, float* dst) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    a += __shfl_xor(a, off);
+    b += __shfl_xor(b, off);
+    c += __shfl_xor(c, off);
+  }
+  const int tid = threadIdx.x, w = tid >> 6;
+  lds_barrier();
+  if ((tid & 63) == 0) {
+    sm[4 * w] = a;
+    sm[4 * w + 1] = b;
+    sm[4 * w + 2] = c;
+  }
+  lds_barrier();
+  if (tid == 0) {
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+    for (int i = 0; i < ROWS / 64; ++i) {
+      s0 += sm[4 * i];
+      s1 += sm[4 * i + 1];
+      s2 += sm[4 * i + 2];
+    }
+    dst[0] = s0;
+    dst[1] = s1;
+    dst[2] = s2;
+  }
+}
+
 template <int ROWS>
 __device__ __forceinline__ void store_ld(float* ld_out, int64_t row0, int tid, int nrows, float v) {
   if (tid < nrows) ld_out[row0 + tid] = v;
@@ -130,7 +193,8 @@ __global__ __launch_bounds__(ROWS, WPE) void k_valu(
     const float* __restrict__ Wg, const int32_t* __restrict__ qtab,
     const int32_t* __restrict__ lflag, const float* __restrict__ in, float* __restrict__ out,
     float* __restrict__ ld_out, float* __restrict__ all, int64_t B, int L, int scale, int shift,
-    int any_perm, int vec_io) {
+    int any_perm, int vec_io, const int64_t* __restrict__ yl, float* __restrict__ loss_part,
+    int kind, float det) {
   using T = typename RowT<RW>::type;
   constexpr int TR = ROWS * RW;  // rows per tile
   constexpr int TF = TR * D;     // floats per tile
@@ -185,6 +249,7 @@ __global__ __launch_bounds__(ROWS, WPE) void k_valu(
   if constexpr (PERSIST) {
     if (vec && tile < nfull) prefetch(tile);
   }
+  float lt0 = 0.f, lt1 = 0.f, lt2 = 0.f;  // fused eval loss (calibrators.py:297-317)
 
   for (; tile < ntiles; tile += stride) {
     const int64_t row0 = tile * TR;
@@ -244,14 +309,27 @@ __global__ __launch_bounds__(ROWS, WPE) void k_valu(
       else store_rows<D, ROWS, false>(out + row0 * D, sm, v, nrows, vec);
     }
     if (ld_out) store_ld<ROWS>(ld_out, row0, tid, nrows, ld);
+    if (loss_part) {
+#pragma unroll
+      for (int q = 0; q < RW; ++q) {
+        const int64_t row = row0 + tid + q * ROWS;
+        if (row < B) {
+          float z[D];
+#pragma unroll
+          for (int j = 0; j < D; ++j) z[j] = odd ? comp(v[D - 1 - j], q) : comp(v[j], q);
+          row_loss<D>(z, comp(ld, q), (int)yl[row], kind, det, lt0, lt1, lt2);
+        }
+      }
+    }
   }
+  if (loss_part) block_sum3<ROWS>(lt0, lt1, lt2, smem, loss_part + (int64_t)blockIdx.x * 4);
 }
 
 // ---------------------------------------------------------------------------
 // instantiation table
 // ---------------------------------------------------------------------------
 using KFn = void (*)(const float*, const int32_t*, const int32_t*, const float*, float*, float*,
-                     float*, int64_t, int, int, int, int, int);
+                     float*, int64_t, int, int, int, int, int, const int64_t*, float*, int, float);
 
 struct Variant {
   KFn fn[2][2];  // [inverse][strict]
@@ -345,12 +423,8 @@ int valu_supported(const Shape& s) {
   return -1;
 }
 
-int valu_run(const Shape& s, const void* prepared, const float* in, float* out, float* ld,
-             float* all, int64_t B, bool inverse, hipStream_t st) {
-  if (s.valu_id < 0) return CNF_ERR_UNSUPPORTED;
-  if (B == 0) return CNF_OK;
+static const Variant* pick_variant(const Shape& s, int64_t B) {
   const Entry& e = kTable[s.valu_id];
-  if (e.nf != s.valu_net_floats) return CNF_ERR_DESC;  // host/device layout disagree
   const bool lds_fits =
       (size_t)256 * 2 * s.D * 4 + (size_t)s.L * s.nets * s.valu_net_floats * 4 <= 64 * 1024;
   const Variant* var = (B > kLargeBatch || !lds_fits) ? &e.large : &e.small;
@@ -359,6 +433,33 @@ int valu_run(const Shape& s, const void* prepared, const float* in, float* out, 
     const int k = std::atoi(xv);
     if (k >= 0 && k < (int)(sizeof(kExp) / sizeof(kExp[0]))) var = &kExp[k];
   }
+  return var;
+}
+
+static int64_t blocks_for(const Shape& s, const Variant* var, KFn fn, int64_t B) {
+  const int64_t tr = (int64_t)var->rows * var->rw;
+  int64_t nblk = (B + tr - 1) / tr;
+  if (var->persist) {
+    const int64_t cap = (int64_t)cu_count() * resident_blocks(fn, var->rows);
+    if (nblk > cap) nblk = cap;
+  }
+  return nblk;
+}
+
+int valu_loss_blocks(const Shape& s, int64_t B) {
+  if (s.valu_id < 0) return -1;
+  const Variant* var = pick_variant(s, B);
+  return (int)blocks_for(s, var, var->fn[0][s.strict ? 1 : 0], B);
+}
+
+int valu_run(const Shape& s, const void* prepared, const float* in, float* out, float* ld,
+             float* all, int64_t B, bool inverse, hipStream_t st, const int64_t* y,
+             float* loss_part, int kind, float det) {
+  if (s.valu_id < 0) return CNF_ERR_UNSUPPORTED;
+  if (B == 0) return CNF_OK;
+  const Entry& e = kTable[s.valu_id];
+  if (e.nf != s.valu_net_floats) return CNF_ERR_DESC;  // host/device layout disagree
+  const Variant* var = pick_variant(s, B);
   const char* base = static_cast<const char*>(prepared);
   const int32_t* fwd_q = reinterpret_cast<const int32_t*>(base);
   const int32_t* inv_q = fwd_q + s.L * s.D;
@@ -368,17 +469,13 @@ int valu_run(const Shape& s, const void* prepared, const float* in, float* out, 
   int vec = al(in) && al(out) && al(all);
   KFn fn = var->fn[inverse ? 1 : 0][s.strict ? 1 : 0];
   const int64_t tr = (int64_t)var->rows * var->rw;
-  int64_t nblk = (B + tr - 1) / tr;
-  if (var->persist) {
-    const int64_t cap = (int64_t)cu_count() * resident_blocks(fn, var->rows);
-    if (nblk > cap) nblk = cap;
-  }
+  const int64_t nblk = blocks_for(s, var, fn, B);
   size_t lds = (size_t)tr * s.D * 4;
   if (var->wl) lds += (size_t)s.L * s.nets * s.valu_net_floats * 4;
   if (lds > 160 * 1024) return CNF_ERR_UNSUPPORTED;
   hipLaunchKernelGGL(fn, dim3((unsigned)nblk), dim3(var->rows), lds, st, W,
                      inverse ? inv_q : fwd_q, flags, in, out, ld, all, B, s.L, s.scale, s.shift,
-                     s.any_perm ? 1 : 0, vec);
+                     s.any_perm ? 1 : 0, vec, y, loss_part, kind, det);
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) {
     set_hip_error(err);

@@ -470,6 +470,13 @@ int partial_stride(const Shape& s) { return (int)(((s.layer_floats * s.L + 3) + 
 
 }  // namespace
 
+int reduce_partials(const float* partials, int nblk, int PS, int P, float* grads, float* terms,
+                    hipStream_t st) {
+  hipLaunchKernelGGL(k_reduce, dim3((unsigned)((P + 3 + 255) / 256)), dim3(256), 0, st,
+                     partials, nblk, PS, P, grads, terms);
+  return CNF_OK;
+}
+
 int vjp_workspace(const Shape& s, int64_t B, size_t* bytes) {
   const VEntry* e = find_entry(s);
   if (!e || lds_bytes(s, *e) > 64 * 1024) return CNF_ERR_UNSUPPORTED;

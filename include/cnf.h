@@ -98,9 +98,20 @@ int cnf_forward(const cnf_desc* desc, const void* prepared, const float* x, floa
 int cnf_inverse(const cnf_desc* desc, const void* prepared, const float* z, float* x,
                 float* logdet, float* x_all, int64_t B, void* stream);
 
-/* Loss kinds for cnf_loss_vjp. */
+/* Loss kinds for cnf_forward_loss / cnf_loss_vjp. */
 #define CNF_LOSS_CAL 0  /* -mean(log(softmax(z_L)[y] + 1e-7) + ld)   calibrators.py:287-291 */
 #define CNF_LOSS_CE 1   /* CE(z_L, y) - det * mean(ld)               run_experiment3D.py:107 */
+
+/* Fused forward + log-det + loss terms (the eval pass of TorchFlowCalibrator.fit,
+ * calibrators.py:297-317; the per-step NLL of a sharded batch):
+ *   loss_terms[3]  {sum of per-row loss, sum of ce, sum of ld} over the B rows
+ *   z, logdet      as cnf_forward, each may be NULL
+ * Deterministic fixed-order reduction.  Narrow flows only (valu-fused family). */
+int cnf_forward_loss_workspace_bytes(const cnf_desc* desc, int64_t B, size_t* bytes);
+int cnf_forward_loss(const cnf_desc* desc, const void* prepared, const float* x,
+                     const int64_t* y, int32_t loss_kind, float det, float* z, float* logdet,
+                     float* loss_terms, int64_t B, void* workspace, size_t workspace_bytes,
+                     void* stream);
 
 /* Workspace bytes cnf_vjp / cnf_loss_vjp need for a batch of B rows. */
 int cnf_vjp_workspace_bytes(const cnf_desc* desc, int64_t B, size_t* bytes);

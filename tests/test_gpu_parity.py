@@ -183,3 +183,25 @@ def test_nonaligned_input_view():
         z, ld = flow.transform(x)
     ozs, old = O.flow_forward(_oracle_layers(flow), x.cpu().numpy())
     assert rel_err(z.cpu().numpy(), ozs[-1]) <= TOL
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+def test_fused_forward_loss_matches_oracle(kind):
+    flow = _make_flow(10, 6, [5, 5], 0.1, 9)
+    stack = flow._native_stack()
+    for B in (1, 1000, 1 << 20):
+        x = _logits(B, 10, 11)
+        y = torch.randint(0, 10, (B,), device=DEV, generator=torch.Generator(device=DEV).manual_seed(5))
+        terms, z, ld = stack.forward_loss(x, y, kind=kind, det=0.5, want_outputs=True)
+        with torch.no_grad():
+            z2, ld2 = flow.transform(x)
+        assert torch.equal(z, z2) and torch.equal(ld, ld2.reshape(-1))
+        lsm = torch.log_softmax(z.double(), dim=1)
+        lpy = lsm.gather(1, y.view(-1, 1)).squeeze(1)
+        ce = -torch.log(torch.exp(lpy) + 1e-7) if kind == 0 else -lpy
+        loss = ce - (1.0 if kind == 0 else 0.5) * ld.double()
+        ref = torch.stack([loss.sum(), ce.sum(), ld.double().sum()]).cpu().numpy()
+        got = terms.double().cpu().numpy()
+        assert np.all(np.abs(got - ref) <= 1e-5 * (np.abs(ref) + B)), (got, ref)
+        t2, _, _ = stack.forward_loss(x, y, kind=kind, det=0.5)
+        assert torch.equal(terms, t2), "non-deterministic reduction"
