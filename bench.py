@@ -123,7 +123,7 @@ class Runner:
                                                            ctypes.byref(n))
             if st != 0:
                 raise RuntimeError("cnf_forward_loss unsupported for this shape: %d" % st)
-            self.ws = torch.empty(max(n.value, 16), dtype=torch.uint8, device=device)
+            self.ws = torch.zeros(max(n.value, 16), dtype=torch.uint8, device=device)
             self.ws_bytes = n.value
         self.i = 0
 

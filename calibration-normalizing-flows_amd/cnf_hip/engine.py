@@ -150,7 +150,7 @@ class CouplingStack:
                                                         ctypes.c_int64(B), ctypes.byref(n)))
         ws = self._loss_ws.get(dev)
         if ws is None or ws.numel() < n.value:
-            ws = torch.empty(max(n.value, 16), dtype=torch.uint8, device=dev)
+            ws = torch.zeros(max(n.value, 16), dtype=torch.uint8, device=dev)  # ticket = 0
             self._loss_ws[dev] = ws
         terms = torch.empty(3, dtype=torch.float32, device=dev)
         z = torch.empty_like(x) if want_outputs else None

@@ -167,7 +167,8 @@ int cnf_forward_loss_workspace_bytes(const cnf_desc* desc, int64_t B, size_t* by
   if (B < 0) return CNF_ERR_BATCH;
   if (s.family != Family::kValu) return CNF_ERR_UNSUPPORTED;
   const int nb = B > 0 ? valu_loss_blocks(s, B) : 0;
-  *bytes = (size_t)(nb > 0 ? nb : 1) * 4 * sizeof(float);
+  // [ticket: 16 B][per-block partials: 4 floats each]
+  *bytes = (size_t)(1 + (nb > 0 ? nb : 1)) * 4 * sizeof(float);
   return CNF_OK;
 }
 
@@ -188,15 +189,14 @@ int cnf_forward_loss(const cnf_desc* desc, const void* prepared, const float* x,
   if (!workspace || workspace_bytes < need) return CNF_ERR_NULL;
   auto mis = [](const void* p) { return p && (reinterpret_cast<uintptr_t>(p) & 3); };
   if (mis(x) || mis(z) || mis(logdet)) return CNF_ERR_ALIGN;
-  float* part = static_cast<float*>(workspace);
-  int nb = 0;
+  float* ws = static_cast<float*>(workspace);
   if (B > 0) {
-    nb = valu_loss_blocks(s, B);
-    st = valu_run(s, prepared, x, z, logdet, nullptr, B, false, (hipStream_t)stream, y, part,
-                  loss_kind, det);
+    st = valu_run(s, prepared, x, z, logdet, nullptr, B, false, (hipStream_t)stream, y, ws,
+                  loss_kind, det, loss_terms);
     if (st != CNF_OK) return st;
+  } else {
+    hipMemsetAsync(loss_terms, 0, 3 * sizeof(float), (hipStream_t)stream);
   }
-  reduce_partials(part, nb, 4, 0, nullptr, loss_terms, (hipStream_t)stream);
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) {
     set_hip_error(err);

@@ -60,7 +60,8 @@ void set_hip_error(hipError_t e);
 int valu_supported(const Shape& s);  // -> valu_id or -1
 int valu_run(const Shape& s, const void* prepared, const float* in, float* out, float* ld,
              float* all, int64_t B, bool inverse, hipStream_t st, const int64_t* y = nullptr,
-             float* loss_part = nullptr, int kind = 0, float det = 0.f);
+             float* loss_ws = nullptr, int kind = 0, float det = 0.f,
+             float* loss_terms = nullptr);
 int valu_loss_blocks(const Shape& s, int64_t B);  // per-block loss partials of the fused eval
 // sum partials[b][i] over b in block order: grads[i] (i < P), terms[i - P] (i < P + 3)
 int reduce_partials(const float* partials, int nblk, int PS, int P, float* grads, float* terms,

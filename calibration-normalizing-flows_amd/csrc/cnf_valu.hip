@@ -125,13 +125,13 @@ __device__ __forceinline__ void row_loss(const float* z, float ld, int y, int ki
   float se = 0.f, zy = z[0];
 #pragma unroll
   for (int j = 0; j < D; ++j) {
-    se += expf(z[j] - m);
-    zy = (j == y) ? z[j] : zy;
+    se += __expf(z[j] - m);
+    zy = (j == y) ? opaque(z[j]) : zy;
   }
-  const float lpy = zy - (m + logf(se));
+  const float lpy = zy - (m + __logf(se));
   float ce, loss;
   if (kind == CNF_LOSS_CAL) {
-    ce = -logf(expf(lpy) + 1e-7f);
+    ce = -__logf(__expf(lpy) + 1e-7f);
     loss = ce - ld;
   } else {
     ce = -lpy;
@@ -142,9 +142,19 @@ __device__ __forceinline__ void row_loss(const float* z, float ld, int y, int ki
   t2 += ld;
 }
 
-// Block sum of three per-thread values in a fixed order -> dst[0..2].
+// Block sum of three per-thread values in a fixed order -> part[blockIdx]; the
+// block that arrives last (device-scope ticket) adds every block's partial in
+// block order and writes terms[0..2] -- deterministic, one launch.  Hand-off
+// per cdna_hip_programming.md Guideline 16, write-through form: the partials
+// are stored sc1 (agent-scope relaxed atomic stores), drained with vmcnt(0),
+// then a relaxed agent ticket add; the last arriver reads every partial with
+// sc1 loads.  No release fence: on this kernel it would write back the
+// whole XCD L2 (every block's freshly written z tile) once per block.  The
+// last arriver resets the ticket for the next call (the workspace starts
+// zeroed).
 template <int ROWS>
-__device__ __forceinline__ void block_sum3(float a, float b, float c, float* sm, float* dst) {
+__device__ __forceinline__ void block_sum3(float a, float b, float c, float* sm, float* part,
+                                           unsigned* ticket, float* terms, int nblk) {
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) {
     a += __shfl_xor(a, off);
@@ -166,9 +176,42 @@ __device__ __forceinline__ void block_sum3(float a, float b, float c, float* sm,
       s1 += sm[4 * i + 1];
       s2 += sm[4 * i + 2];
     }
-    dst[0] = s0;
-    dst[1] = s1;
-    dst[2] = s2;
+    float* dst = part + (int64_t)blockIdx.x * 4;
+    __hip_atomic_store(dst, s0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(dst + 1, s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(dst + 2, s2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+    sm[64] = t == (unsigned)(nblk - 1) ? 1.f : 0.f;
+  }
+  __syncthreads();
+  if (sm[64] == 0.f) return;  // block-uniform
+  float r0 = 0.f, r1 = 0.f, r2 = 0.f;
+  for (int bb = tid; bb < nblk; bb += ROWS) {
+    const float* src = part + (int64_t)bb * 4;
+    r0 += __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    r1 += __hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    r2 += __hip_atomic_load(src + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  sm[tid] = r0;
+  sm[ROWS + tid] = r1;
+  sm[2 * ROWS + tid] = r2;
+  __syncthreads();
+  for (int h = ROWS / 2; h >= 1; h >>= 1) {
+    if (tid < h) {
+      sm[tid] += sm[tid + h];
+      sm[ROWS + tid] += sm[ROWS + tid + h];
+      sm[2 * ROWS + tid] += sm[2 * ROWS + tid + h];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    terms[0] = sm[0];
+    terms[1] = sm[ROWS];
+    terms[2] = sm[2 * ROWS];
+    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -194,7 +237,7 @@ __global__ __launch_bounds__(ROWS, WPE) void k_valu(
     const int32_t* __restrict__ lflag, const float* __restrict__ in, float* __restrict__ out,
     float* __restrict__ ld_out, float* __restrict__ all, int64_t B, int L, int scale, int shift,
     int any_perm, int vec_io, const int64_t* __restrict__ yl, float* __restrict__ loss_part,
-    int kind, float det) {
+    int kind, float det, unsigned* __restrict__ ticket, float* __restrict__ loss_terms) {
   using T = typename RowT<RW>::type;
   constexpr int TR = ROWS * RW;  // rows per tile
   constexpr int TF = TR * D;     // floats per tile
@@ -322,14 +365,15 @@ __global__ __launch_bounds__(ROWS, WPE) void k_valu(
       }
     }
   }
-  if (loss_part) block_sum3<ROWS>(lt0, lt1, lt2, smem, loss_part + (int64_t)blockIdx.x * 4);
+  if (loss_part) block_sum3<ROWS>(lt0, lt1, lt2, smem, loss_part, ticket, loss_terms, gridDim.x);
 }
 
 // ---------------------------------------------------------------------------
 // instantiation table
 // ---------------------------------------------------------------------------
 using KFn = void (*)(const float*, const int32_t*, const int32_t*, const float*, float*, float*,
-                     float*, int64_t, int, int, int, int, int, const int64_t*, float*, int, float);
+                     float*, int64_t, int, int, int, int, int, const int64_t*, float*, int, float,
+                     unsigned*, float*);
 
 struct Variant {
   KFn fn[2][2];  // [inverse][strict]
@@ -386,6 +430,9 @@ const Variant kExp[] = {
     CNF_VARIANT(10, 5, 5, 2, 256, false, 4, true, true),                  // 2: = small
     CNF_VARIANT_X(10, 5, 5, 2, 256, false, 4, true, false, false, true),  // 3: chunked, 2/lane
     CNF_VARIANT(10, 5, 5, 4, 256, false, 2, true, true),                  // 4: LDS, 4/lane
+    CNF_VARIANT(10, 5, 5, 2, 256, false, 4, true, false),                 // 5: scalar, 2/lane
+    CNF_VARIANT(10, 5, 5, 2, 128, false, 4, true, true),                  // 6: LDS, 2/lane, 128 thr
+    CNF_VARIANT(10, 5, 5, 1, 256, false, 6, true, true),                  // 7: LDS, 1/lane
 };
 
 int cu_count() {
@@ -454,7 +501,7 @@ int valu_loss_blocks(const Shape& s, int64_t B) {
 
 int valu_run(const Shape& s, const void* prepared, const float* in, float* out, float* ld,
              float* all, int64_t B, bool inverse, hipStream_t st, const int64_t* y,
-             float* loss_part, int kind, float det) {
+             float* loss_ws, int kind, float det, float* loss_terms) {
   if (s.valu_id < 0) return CNF_ERR_UNSUPPORTED;
   if (B == 0) return CNF_OK;
   const Entry& e = kTable[s.valu_id];
@@ -471,11 +518,13 @@ int valu_run(const Shape& s, const void* prepared, const float* in, float* out, 
   const int64_t tr = (int64_t)var->rows * var->rw;
   const int64_t nblk = blocks_for(s, var, fn, B);
   size_t lds = (size_t)tr * s.D * 4;
+  if (lds < (size_t)3 * var->rows * 4 + 4 * 65) lds = (size_t)3 * var->rows * 4 + 4 * 65;
   if (var->wl) lds += (size_t)s.L * s.nets * s.valu_net_floats * 4;
   if (lds > 160 * 1024) return CNF_ERR_UNSUPPORTED;
   hipLaunchKernelGGL(fn, dim3((unsigned)nblk), dim3(var->rows), lds, st, W,
                      inverse ? inv_q : fwd_q, flags, in, out, ld, all, B, s.L, s.scale, s.shift,
-                     s.any_perm ? 1 : 0, vec, y, loss_part, kind, det);
+                     s.any_perm ? 1 : 0, vec, y, loss_ws ? loss_ws + 4 : nullptr, kind, det,
+                     reinterpret_cast<unsigned*>(loss_ws), loss_terms);
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) {
     set_hip_error(err);

@@ -193,11 +193,21 @@ __device__ __forceinline__ void mlp(const float* __restrict__ w, const T* c, T p
 template <int D, bool O>
 __device__ __forceinline__ constexpr int R(int j) { return O ? D - 1 - j : j; }
 
+// Opaque copy: keeps LLVM from turning a select chain over an array into a
+// dynamically indexed load (which demotes the array to scratch memory).
+template <class T>
+__device__ __forceinline__ T opaque(T a) {
+  asm("" : "+v"(a));
+  return a;
+}
+
 template <int D, class T>
 __device__ __forceinline__ T pick(const T* v, int idx) {
-  T r = v[0];
+  // opaque(): without it LLVM folds the chain into v[idx] and keeps v in
+  // scratch (measured: ~120 B/row of extra HBM writes on cfg2).
+  T r = opaque(v[0]);
 #pragma unroll
-  for (int k = 1; k < D; ++k) r = (idx == k) ? v[k] : r;
+  for (int k = 1; k < D; ++k) r = (idx == k) ? opaque(v[k]) : r;
   return r;
 }
 

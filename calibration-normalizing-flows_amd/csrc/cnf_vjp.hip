@@ -238,7 +238,7 @@ __global__ __launch_bounds__(kVRows) void k_vjp(
         const int yy = valid ? (int)y[row] : 0;
         float zy = z[0];
 #pragma unroll
-        for (int j = 1; j < D; ++j) zy = (j == yy) ? z[j] : zy;
+        for (int j = 1; j < D; ++j) zy = (j == yy) ? opaque(z[j]) : zy;
         const float lpy = zy - lse;
         float coef, ce_term, loss_row;
         if (kind == CNF_LOSS_CAL) {  // -(log(softmax(z)[y] + 1e-7) + ld)
@@ -416,15 +416,60 @@ __global__ __launch_bounds__(kVRows) void k_vjp(
   }
 }
 
-// grads[p] = sum over blocks (in block order) of the partials; terms likewise.
-__global__ void k_reduce(const float* __restrict__ partials, int nblk, int PS, int P,
-                         float* __restrict__ grads, float* __restrict__ terms) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= P + 3) return;
+// Fixed-order reductions of the per-block partials partials[b][0..NE) (row
+// stride PS) -- deterministic: every entry is always summed in the same tree.
+//
+// Many entries (weight gradients): a block owns 64 consecutive entries and
+// its 4 waves split the blocks b = g, g+4, ... (coalesced 256-B rows); the 4
+// group sums are then added in group order.
+__global__ __launch_bounds__(256) void k_reduce_cols(const float* __restrict__ partials, int nblk,
+                                                     int PS, int NE, float* __restrict__ out) {
+  __shared__ float red[256];
+  const int e = blockIdx.x * 64 + (threadIdx.x & 63), g = threadIdx.x >> 6;
   float s = 0.f;
-  for (int b = 0; b < nblk; ++b) s += partials[(int64_t)b * PS + i];
-  if (i < P) grads[i] = s;
-  else if (terms) terms[i - P] = s;
+  if (e < NE) {
+    int b = g;
+    for (; b + 12 < nblk; b += 16) {
+      const float a0 = partials[(int64_t)b * PS + e], a1 = partials[(int64_t)(b + 4) * PS + e];
+      const float a2 = partials[(int64_t)(b + 8) * PS + e];
+      const float a3 = partials[(int64_t)(b + 12) * PS + e];
+      s += a0;
+      s += a1;
+      s += a2;
+      s += a3;
+    }
+    for (; b < nblk; b += 4) s += partials[(int64_t)b * PS + e];
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (g == 0 && e < NE) out[e] = ((red[threadIdx.x] + red[threadIdx.x + 64]) +
+                                  red[threadIdx.x + 128]) + red[threadIdx.x + 192];
+}
+
+// Few entries (the 3 loss sums): one block, thread t adds blocks t, t+256, ...
+// then a fixed LDS tree.
+__global__ __launch_bounds__(256) void k_reduce_rows(const float* __restrict__ partials,
+                                                     int nblk, int PS, int E0, int NE,
+                                                     float* __restrict__ out) {
+  __shared__ float red[4][256];
+  const int t = threadIdx.x;
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int b = t; b < nblk; b += 256) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (e < NE) s[e] += partials[(int64_t)b * PS + E0 + e];
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) red[e][t] = s[e];
+  __syncthreads();
+  for (int w = 128; w >= 1; w >>= 1) {
+    if (t < w) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) red[e][t] += red[e][t + w];
+    }
+    __syncthreads();
+  }
+  if (t < NE) out[t] = red[t][0];
 }
 
 using VFn = void (*)(const float*, const int32_t*, const int32_t*, const int32_t*, const float*,
@@ -472,8 +517,12 @@ int partial_stride(const Shape& s) { return (int)(((s.layer_floats * s.L + 3) + 
 
 int reduce_partials(const float* partials, int nblk, int PS, int P, float* grads, float* terms,
                     hipStream_t st) {
-  hipLaunchKernelGGL(k_reduce, dim3((unsigned)((P + 3 + 255) / 256)), dim3(256), 0, st,
-                     partials, nblk, PS, P, grads, terms);
+  if (P > 0)
+    hipLaunchKernelGGL(k_reduce_cols, dim3((unsigned)((P + 63) / 64)), dim3(256), 0, st,
+                       partials, nblk, PS, P, grads);
+  if (terms)
+    hipLaunchKernelGGL(k_reduce_rows, dim3(1), dim3(256), 0, st, partials, nblk, PS, P, 3,
+                       terms);
   return CNF_OK;
 }
 
@@ -511,8 +560,7 @@ int vjp_run(const Shape& s, const void* prepared, const float* x, const int64_t*
                        iq, flags, x, y, gz, gz_all, gld, dx, partials, B, s.L, s.scale, s.shift,
                        s.any_perm ? 1 : 0, kind, det, grad_scale, P, PS);
   }
-  hipLaunchKernelGGL(k_reduce, dim3((unsigned)((P + 3 + 255) / 256)), dim3(256), 0, st,
-                     partials, (int)nblk, PS, P, grads, loss_terms);
+  reduce_partials(partials, (int)nblk, PS, P, grads, loss_terms, st);
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) {
     set_hip_error(err);

@@ -91,6 +91,13 @@ class Flow(nn.Module):
         self._stack = None
         self._stack_key = None
 
+    def __getstate__(self):
+        # the native binding (ctypes descriptor, device blobs) is rebuilt lazily
+        st = self.__dict__.copy()
+        st["_stack"] = None
+        st["_stack_key"] = None
+        return st
+
     # -- native plumbing --------------------------------------------------
     def _native_stack(self):
         key = (tuple(id(ly) for ly in self.layers), self._strict())
@@ -226,6 +233,11 @@ class NvpCouplingLayer(nn.Module):
                                      requires_grad=False)
             self.rev_perm = nn.Parameter(torch.as_tensor(rev[None], dtype=torch.long),
                                          requires_grad=False)
+
+    def __getstate__(self):
+        st = self.__dict__.copy()
+        st["_stack"] = None
+        return st
 
     def _native(self, x, inverse):
         if not _native_eligible([self], x):

@@ -11,16 +11,22 @@ import torch  # noqa: E402
 
 import bench  # noqa: E402
 
-VARIANTS = [int(v) for v in os.environ.get("VARIANTS", "0,1,2,3,4").split(",")]
+VARIANTS = [int(v) for v in os.environ.get("VARIANTS", "1,2,4,5,6,7").split(",")]
 
 
 def main():
     dev = torch.device("cuda:0")
-    for name, wl, allo in (("cfg2", bench.WORKLOADS["cfg2"], False),
-                           ("cfg5", bench.WORKLOADS["cfg5"], False),
-                           ("cfg2_all", bench.WORKLOADS["cfg2"], True),
-                           ("cfg2_8M", dict(bench.WORKLOADS["cfg2"], B=8 << 20), False)):
-        r = bench.Runner(dict(wl), dev, 1.5e9, all_outputs=allo)
+    cases = (("cfg2_loss", bench.WORKLOADS["cfg2"], False, "loss"),
+             ("cfg2", bench.WORKLOADS["cfg2"], False, "forward"),
+             ("cfg5", bench.WORKLOADS["cfg5"], False, "forward"),
+             ("cfg2_all", bench.WORKLOADS["cfg2"], True, "forward"),
+             ("cfg2_8M", dict(bench.WORKLOADS["cfg2"], B=8 << 20), False, "forward"),
+             ("cfg2_8M_loss", dict(bench.WORKLOADS["cfg2"], B=8 << 20), False, "loss"))
+    only = os.environ.get("CASES")
+    for name, wl, allo, mode in cases:
+        if only and name not in only.split(","):
+            continue
+        r = bench.Runner(dict(wl), dev, 1.5e9, all_outputs=allo, mode=mode)
         res = {v: [] for v in VARIANTS}
         for rnd in range(5):
             for v in VARIANTS:

@@ -1,7 +1,8 @@
 #!/bin/bash
-# One GPU-box session: smoke, GPU tests, bench, rocprofv3 kernel-trace summary.
-# Every GPU step has its own time limit; a fault/abort/timeout ends the script
-# (exit codes other than 0 and 1).  Usage: bash tools/gpu_check.sh [tag]
+# One GPU-box session: smoke, GPU tests, bench, rocprofv3 kernel-trace summary,
+# and the PMC traffic passes for the bench kernel.  Every GPU step has its own
+# time limit; a fault/abort/timeout ends the script (exit codes other than 0, 1).
+# Usage: bash tools/gpu_check.sh [tag]
 set -u
 TAG=${1:-r01}
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -13,11 +14,12 @@ run() {
   timeout -k 10 "$@" > gpurun_out/$name.log 2>&1
   local rc=$?
   echo "$name rc=$rc ($(( $(date +%s) - t0 ))s)"
-  tail -n 5 gpurun_out/$name.log
+  tail -n ${TAILN:-5} gpurun_out/$name.log | grep -v amdgpu.ids
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
 }
 run smoke 400 python -c "import __graft_entry__ as g; g.smoke()"
-run pytest_gpu 900 python -m pytest tests -m gpu -x -q
-run bench 600 python bench.py
+run pytest_gpu 900 python -m pytest tests -m gpu -q
+TAILN=2 run bench 600 python bench.py
 run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python bench.py --steps 100 --no-cpu-baseline --no-variants
+run pmc 600 bash tools/gpu_pmc.sh $TAG cfg2 "--launches 30" "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SMEM GRBM_GUI_ACTIVE"
 exit 0

@@ -15,11 +15,13 @@ ap.add_argument("--workload", default="cfg2")
 ap.add_argument("--launches", type=int, default=40)
 ap.add_argument("--all", action="store_true")
 ap.add_argument("--batch", type=int, default=0)
+ap.add_argument("--mode", default="loss", choices=["loss", "forward"])
 a = ap.parse_args()
 w = dict(bench.WORKLOADS[a.workload])
 if a.batch:
     w["B"] = a.batch
-r = bench.Runner(w, torch.device("cuda:0"), 1.5e9, all_outputs=a.all)
+mode = a.mode if (w["D"] <= 16 and not w["inverse"] and not a.all) else "forward"
+r = bench.Runner(w, torch.device("cuda:0"), 1.5e9, all_outputs=a.all, mode=mode)
 for _ in range(a.launches):
     r.step()
 torch.cuda.synchronize()
