@@ -65,6 +65,18 @@ int derive_shape(const cnf_desc* d, Shape* s) {
       off += ((int64_t)nout * ((nin + 3) & ~3) + ((nout + 3) & ~3) + 15) & ~15;
     }
     s->valu_net_floats = off;
+    s->sp_ok = true;
+    off = 0;
+    for (int i = 0; i < s->n_lin; ++i) {
+      const int nin = i == 0 ? s->DC : s->units[i];
+      const int nout = i == s->n_lin - 1 ? s->DT : s->units[i + 1];
+      const int64_t f = ((int64_t)nout * nin + nout + 15) & ~15;
+      if (f > 32) s->sp_ok = false;
+      s->sp_lin_off[i] = off;
+      off += f;
+    }
+    s->sp_net_floats = off;
+    s->sp_region = s->valu_net_floats * s->nets * s->L;
   } else {
     s->family = Family::kTile;
     int st = tile_configure(s);
@@ -119,8 +131,10 @@ int cnf_prepared_bytes(const cnf_desc* desc, size_t* bytes) {
   int st = derive_shape(desc, &s);
   if (st != CNF_OK) return st;
   if (!bytes) return CNF_ERR_NULL;
-  const int64_t wf = s.family == Family::kTile ? s.tile_layer_floats * s.L
-                                                : s.valu_net_floats * s.nets * s.L;
+  const int64_t wf = s.family == Family::kTile
+                       ? s.tile_layer_floats * s.L
+                       : s.valu_net_floats * s.nets * s.L +
+                             (s.sp_ok ? s.sp_net_floats * s.nets * s.L : 0);
   // +256: scalar-cache prefetch reads whole 64-B lines past the last weight
   *bytes = (size_t)(idx_bytes(s) + wf * 4 + 256);
   return CNF_OK;
@@ -167,7 +181,7 @@ int cnf_forward_loss_workspace_bytes(const cnf_desc* desc, int64_t B, size_t* by
   if (B < 0) return CNF_ERR_BATCH;
   if (s.family != Family::kValu) return CNF_ERR_UNSUPPORTED;
   const int nb = B > 0 ? valu_loss_blocks(s, B) : 0;
-  // [ticket: 16 B][per-block partials: 4 floats each]
+  // [16 B reserved][per-block partials: 4 floats each]
   *bytes = (size_t)(1 + (nb > 0 ? nb : 1)) * 4 * sizeof(float);
   return CNF_OK;
 }
@@ -195,7 +209,11 @@ int cnf_forward_loss(const cnf_desc* desc, const void* prepared, const float* x,
                   loss_kind, det, loss_terms);
     if (st != CNF_OK) return st;
   } else {
-    hipMemsetAsync(loss_terms, 0, 3 * sizeof(float), (hipStream_t)stream);
+    hipError_t e = hipMemsetAsync(loss_terms, 0, 3 * sizeof(float), (hipStream_t)stream);
+    if (e != hipSuccess) {
+      set_hip_error(e);
+      return CNF_ERR_HIP;
+    }
   }
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) {

@@ -34,6 +34,13 @@ struct Shape {
   // VALU compact layout (cnf_valu_common.h): per Linear W[nout][pad4(nin)], b[pad4(nout)]
   int64_t valu_lin_off[kMaxLin] = {};
   int64_t valu_net_floats = 0;
+  // pipelined-scalar layout (cnf_sgpr.hip), appended after the compact region:
+  // per Linear W[nout][nin] + b[nout] (last Linear: nout = DT) padded to 16
+  // floats; sp_ok when every Linear fits 32 floats
+  bool sp_ok = false;
+  int64_t sp_lin_off[kMaxLin] = {};
+  int64_t sp_net_floats = 0;
+  int64_t sp_region = 0;  // float offset of the region in the weights region
   // tile (MFMA) layout
   int NO = 0;                        // last-linear outputs computed: DT (fast) or D (strict)
   int lin_nin[kMaxLin] = {}, lin_nout[kMaxLin] = {}, lin_inoff[kMaxLin] = {};
@@ -63,6 +70,11 @@ int valu_run(const Shape& s, const void* prepared, const float* in, float* out, 
              float* loss_ws = nullptr, int kind = 0, float det = 0.f,
              float* loss_terms = nullptr);
 int valu_loss_blocks(const Shape& s, int64_t B);  // per-block loss partials of the fused eval
+bool sgpr_enabled(const Shape& s);
+int64_t sgpr_blocks(int64_t B);
+int sgpr_run(const Shape& s, const void* prepared, const float* in, float* out, float* ld,
+             float* all, int64_t B, bool inverse, hipStream_t st, const int64_t* y,
+             float* loss_ws, int kind, float det, float* loss_terms);
 // sum partials[b][i] over b in block order: grads[i] (i < P), terms[i - P] (i < P + 3)
 int reduce_partials(const float* partials, int nblk, int PS, int P, float* grads, float* terms,
                     hipStream_t st);

@@ -1,0 +1,275 @@
+// Fused multi-layer coupling kernel, pipelined-scalar-weight form, for the
+// narrow calibration flows whose every conditioner Linear fits 32 floats
+// (W[nout][nin] + b[nout]: the reference default D=10, hidden_size=[5,5],
+// flows/flows.py:71, is three 5x5 Linears per net).
+//
+// Same math and tile/row layout as k_valu (cnf_valu.hip header comment,
+// flows/flows.py:101-126), different weight path: every Linear's block is
+// pulled into SGPRs by two s_load_dwordx16 issued one Linear AHEAD of its use
+// (double-buffered, 64 SGPRs), so
+//   * each FMA takes its weight as an SGPR operand (op_sel picks the half),
+//     with no VGPR copies of weights and no LDS broadcast traffic;
+//   * the scalar-cache round trip of a Linear overlaps the previous Linear's
+//     FMAs instead of stalling the wave once per output neuron.
+// Non-strict only (strict_nan keeps k_valu); shift must be on (NICE: s = 0).
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+
+#include "cnf_internal.h"
+#include "cnf_valu_common.h"
+#include "cnf_valu_io.h"
+
+namespace cnf {
+namespace {
+
+using namespace valu;
+
+// Compile-time SP layout of one net (must match derive_shape's sp_lin_off).
+template <int D, int H1, int H2>
+struct SP {
+  static constexpr int DT = D / 2, DC = D - D / 2;
+  static constexpr int NL = H1 == 0 ? 1 : (H2 == 0 ? 2 : 3);
+  static constexpr int nin(int i) { return i == 0 ? DC : (i == 1 ? H1 : H2); }
+  static constexpr int nout(int i) { return i == NL - 1 ? DT : (i == 0 ? H1 : H2); }
+  static constexpr int fl(int i) { return pad16(nin(i) * nout(i) + nout(i)); }
+  static constexpr int off(int i) { return i == 0 ? 0 : off(i - 1) + fl(i - 1); }
+  static constexpr int NF = off(NL);
+  static constexpr int mx(int i) { return i == NL ? 0 : (fl(i) > mx(i + 1) ? fl(i) : mx(i + 1)); }
+  static constexpr int NC = mx(0) / 16;  // 64-B chunks per buffer
+  static_assert(NC >= 1 && NC <= 2, "Linear block exceeds the 32-float SGPR buffer");
+};
+
+template <int NC>
+struct SW {
+  v16f c[NC];
+  __device__ __forceinline__ float operator[](int i) const { return c[i >> 4][i & 15]; }
+};
+
+// Issue the loads only; swait() is the point the values become usable.  The
+// wait names the buffer as an in/out operand, so no use is scheduled above it.
+template <int NC>
+__device__ __forceinline__ void sissue(SW<NC>& r, const float* p) {
+  if constexpr (NC == 1) {
+    asm volatile("s_load_dwordx16 %0, %1, 0x0" : "=s"(r.c[0]) : "s"(p));
+  } else {
+    asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx16 %1, %2, 0x40"
+                 : "=&s"(r.c[0]), "=s"(r.c[1]) : "s"(p));
+  }
+}
+template <int NC>
+__device__ __forceinline__ void swait(SW<NC>& r) {
+  if constexpr (NC == 1) {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(r.c[0]));
+  } else {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(r.c[0]), "+s"(r.c[1]));
+  }
+}
+
+// y[o] = b[o] + sum_k W[o][k] x[k] from an SGPR block laid out W[NOUT][NIN], b[NOUT]
+template <int NIN, int NOUT, bool RELU, int NC, class T>
+__device__ __forceinline__ void slin(const SW<NC>& w, const T* x, T* y) {
+#pragma unroll
+  for (int o = 0; o < NOUT; ++o) {
+    T a = splat(w[NOUT * NIN + o], T{});
+#pragma unroll
+    for (int k = 0; k < NIN; ++k) a = fmaT(w[o * NIN + k], x[k], a);
+    y[o] = RELU ? relu<false>(a) : a;
+  }
+}
+
+// Linear IDX of the layer's sequence (net-major: s-net Linears, then t-net);
+// the next block (or the next layer's first, wn) is issued before computing.
+template <class S, int NETS, int IDX, class T>
+__device__ __forceinline__ void run_seq(const T* c, T* h1, T* h2, T* s, T* t, SW<S::NC>& cur,
+                                        const float* wl, const float* wn) {
+  if constexpr (IDX < NETS * S::NL) {
+    constexpr int net = IDX / S::NL, i = IDX % S::NL;
+    SW<S::NC> nxt;
+    if constexpr (IDX + 1 < NETS * S::NL)
+      sissue(nxt, wl + ((IDX + 1) / S::NL) * S::NF + S::off((IDX + 1) % S::NL));
+    else
+      sissue(nxt, wn);
+    constexpr bool last = i == S::NL - 1;
+    const T* in = i == 0 ? c : (i == 1 ? h1 : h2);
+    T* out = last ? ((NETS == 2 && net == 0) ? s : t) : (i == 0 ? h1 : h2);
+    slin<S::nin(i), S::nout(i), !last>(cur, in, out);
+    swait(nxt);
+    cur = nxt;
+    run_seq<S, NETS, IDX + 1>(c, h1, h2, s, t, cur, wl, wn);
+  }
+}
+
+// One coupling layer, input in orientation O, output in orientation !O
+// (k_valu's step(), non-strict, weights from the pipelined SGPR buffer).
+template <int D, int H1, int H2, bool INV, bool O, int NETS, class T>
+__device__ __forceinline__ void sp_step(T* v, T& ld, SW<SP<D, H1, H2>::NC>& cur,
+                                        const float* wl, const float* wn, bool perm,
+                                        const int32_t* __restrict__ q) {
+  using S = SP<D, H1, H2>;
+  constexpr int DT = S::DT, DC = S::DC;
+  constexpr bool OC = INV ? !O : O;
+  if constexpr (INV) {
+    if (perm) permute<D, O>(v, q);  // flows/flows.py:115-117
+  }
+  T c[DC];
+#pragma unroll
+  for (int k = 0; k < DC; ++k) c[k] = v[R<D, OC>(DT + k)];
+  T h1[H1 > 0 ? H1 : 1], h2[H2 > 0 ? H2 : 1], s[DT], t[DT];
+  run_seq<S, NETS, 0>(c, h1, h2, s, t, cur, wl, wn);
+#pragma unroll
+  for (int j = 0; j < DT; ++j) {
+    T& x = v[R<D, OC>(j)];
+    if constexpr (NETS == 1) {  // scale=False: s = 0, exp(0) = 1, log-det += 0
+      x = INV ? x - t[j] : x + t[j];
+    } else if constexpr (!INV) {
+      x = fmaV(x, expT<true>(s[j]), t[j]);
+      ld += s[j];
+    } else {
+      x = (x - t[j]) * expT<true>(-s[j]);
+      ld -= s[j];
+    }
+  }
+  if constexpr (!INV) {
+    if (perm) permute<D, O>(v, q);  // flows/flows.py:110-112
+  }
+}
+
+template <int D, int H1, int H2, bool INV, int NETS, int RW, int ROWS>
+__global__ __launch_bounds__(ROWS, 4) void k_sgpr(
+    const float* __restrict__ W, const int32_t* __restrict__ qtab,
+    const int32_t* __restrict__ lflag, const float* __restrict__ in, float* __restrict__ out,
+    float* __restrict__ ld_out, float*, int64_t B, int L, int, int,
+    int any_perm, int vec_io, const int64_t* __restrict__ yl, float* __restrict__ loss_part,
+    int kind, float det, unsigned*, float*) {
+  using S = SP<D, H1, H2>;
+  using T = typename RowT<RW>::type;
+  constexpr int TR = ROWS * RW;
+  constexpr int LF = NETS * S::NF;  // floats per layer
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* sm = smem;
+  const int tid = threadIdx.x;
+  const bool vec = vec_io != 0;
+  const int64_t ntiles = (B + TR - 1) / TR;
+  auto layer_of = [&](int i) { return INV ? L - 1 - i : i; };
+  float lt0 = 0.f, lt1 = 0.f, lt2 = 0.f;
+
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t row0 = tile * TR;
+    const int nrows = (int)((B - row0) < TR ? (B - row0) : TR);
+    SW<S::NC> cur;
+    sissue(cur, W + (int64_t)layer_of(0) * LF);  // lands while the tile loads
+    lds_barrier();
+    tile_load<ROWS>(sm, in + row0 * D, nrows * D, vec);
+    int yv[RW];
+    if (loss_part) load_labels<RW>(yl, row0, tid, ROWS, B, yv);
+    lds_barrier();
+    swait(cur);
+    T v[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) v[k] = get_row<ROWS>(sm, tid, D, k, T{});
+    T ld = splat(0.f, T{});
+    int i = 0;
+    for (; i + 1 < L; i += 2) {
+      const int la = layer_of(i), lb = layer_of(i + 1), lc = layer_of(i + 2 < L ? i + 2 : 0);
+      const bool pa = any_perm && (lflag[la] & kFlagPerm);
+      const bool pb = any_perm && (lflag[lb] & kFlagPerm);
+      sp_step<D, H1, H2, INV, false, NETS>(v, ld, cur, W + (int64_t)la * LF,
+                                           W + (int64_t)lb * LF, pa, qtab + la * D);
+      sp_step<D, H1, H2, INV, true, NETS>(v, ld, cur, W + (int64_t)lb * LF,
+                                          W + (int64_t)lc * LF, pb, qtab + lb * D);
+    }
+    const bool odd = i < L;
+    if (odd) {
+      const int la = layer_of(i);
+      const bool pa = any_perm && (lflag[la] & kFlagPerm);
+      sp_step<D, H1, H2, INV, false, NETS>(v, ld, cur, W + (int64_t)la * LF,
+                                           W + (int64_t)layer_of(0) * LF, pa, qtab + la * D);
+    }
+    if (out) {
+      if (odd) store_rows<D, ROWS, true>(out + row0 * D, sm, v, nrows, vec);
+      else store_rows<D, ROWS, false>(out + row0 * D, sm, v, nrows, vec);
+    }
+    if (ld_out) store_ld<ROWS>(ld_out, row0, tid, nrows, ld);
+    if (loss_part) {
+      if (odd) tile_loss<D, true>(v, ld, yv, kind, det, lt0, lt1, lt2);
+      else tile_loss<D, false>(v, ld, yv, kind, det, lt0, lt1, lt2);
+    }
+  }
+  if (loss_part) block_sum3<ROWS>(lt0, lt1, lt2, smem, loss_part);
+}
+
+using KFn = void (*)(const float*, const int32_t*, const int32_t*, const float*, float*, float*,
+                     float*, int64_t, int, int, int, int, int, const int64_t*, float*, int, float,
+                     unsigned*, float*);
+
+constexpr int kRW = 2, kRows = 256;
+
+struct SEntry {
+  int D, H1, H2;
+  KFn fn[2][2];  // [nets - 1][inverse]
+};
+
+#define CNF_SGPR(D, H1, H2)                                                              \
+  {D, H1, H2,                                                                            \
+   {{k_sgpr<D, H1, H2, false, 1, kRW, kRows>, k_sgpr<D, H1, H2, true, 1, kRW, kRows>},   \
+    {k_sgpr<D, H1, H2, false, 2, kRW, kRows>, k_sgpr<D, H1, H2, true, 2, kRW, kRows>}}}
+
+// every shape of the VALU table whose Linears fit the 32-float buffer
+const SEntry kSTable[] = {
+    CNF_SGPR(2, 5, 5), CNF_SGPR(3, 5, 5), CNF_SGPR(4, 5, 5), CNF_SGPR(5, 5, 5),
+    CNF_SGPR(6, 5, 5), CNF_SGPR(8, 5, 5), CNF_SGPR(10, 5, 5),
+    CNF_SGPR(3, 3, 3), CNF_SGPR(8, 3, 3), CNF_SGPR(10, 3, 3),
+    CNF_SGPR(3, 3, 0), CNF_SGPR(3, 0, 0), CNF_SGPR(10, 0, 0),
+    CNF_SGPR(10, 5, 0), CNF_SGPR(3, 5, 0),
+};
+
+const SEntry* find(const Shape& s) {
+  const int h1 = s.n_lin >= 2 ? s.units[1] : 0, h2 = s.n_lin >= 3 ? s.units[2] : 0;
+  for (const SEntry& e : kSTable)
+    if (e.D == s.D && e.H1 == h1 && e.H2 == h2) return &e;
+  return nullptr;
+}
+
+}  // namespace
+
+// all_outputs (z_all) launches stay on k_valu: the per-layer stores cost this
+// kernel SGPRs it does not have.
+bool sgpr_enabled(const Shape& s) {
+  if (!s.sp_ok || s.strict || !s.shift || !find(s)) return false;
+  const char* e = std::getenv("CNF_SGPR");  // A/B switch: CNF_SGPR=0 keeps k_valu
+  return !(e && e[0] == '0');
+}
+
+int64_t sgpr_blocks(int64_t B) { return (B + kRW * kRows - 1) / (kRW * kRows); }
+
+int sgpr_run(const Shape& s, const void* prepared, const float* in, float* out, float* ld,
+             float* all, int64_t B, bool inverse, hipStream_t st, const int64_t* y,
+             float* loss_ws, int kind, float det, float* loss_terms) {
+  const SEntry* e = find(s);
+  if (!e || !s.sp_ok || all) return CNF_ERR_UNSUPPORTED;  // every-layer outputs: k_valu
+  if (B == 0) return CNF_OK;
+  const char* base = static_cast<const char*>(prepared);
+  const int32_t* fwd_q = reinterpret_cast<const int32_t*>(base);
+  const int32_t* inv_q = fwd_q + s.L * s.D;
+  const int32_t* flags = inv_q + s.L * s.D;
+  const float* W = reinterpret_cast<const float*>(base + idx_bytes(s)) + s.sp_region;
+  auto al = [](const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  const int vec = al(in) && al(out) && al(all);
+  KFn fn = e->fn[s.scale ? 1 : 0][inverse ? 1 : 0];
+  const int64_t nblk = sgpr_blocks(B);
+  size_t lds = (size_t)kRW * kRows * s.D * 4;
+  if (lds < (size_t)3 * kRows * 4 + 4 * 65) lds = (size_t)3 * kRows * 4 + 4 * 65;
+  hipLaunchKernelGGL(fn, dim3((unsigned)nblk), dim3(kRows), lds, st, W, inverse ? inv_q : fwd_q,
+                     flags, in, out, ld, all, B, s.L, s.scale, s.shift, s.any_perm ? 1 : 0, vec,
+                     y, loss_ws ? loss_ws + 4 : nullptr, kind, det, nullptr, nullptr);
+  if (loss_ws) reduce_partials(loss_ws + 4, (int)nblk, 4, 0, nullptr, loss_terms, st);
+  hipError_t err = hipGetLastError();
+  if (err != hipSuccess) {
+    set_hip_error(err);
+    return CNF_ERR_HIP;
+  }
+  return CNF_OK;
+}
+
+}  // namespace cnf

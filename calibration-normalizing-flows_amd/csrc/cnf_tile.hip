@@ -228,7 +228,7 @@ struct PrepSeg {
   const float* W;
   const float* b;
   int64_t dst;  // float offset in the weights region
-  int mode;     // 0: natural copy (W then b), 1: MFMA tiles, 2: compact (VALU)
+  int mode;     // 0: natural copy, 1: MFMA tiles, 2: compact (VALU), 3: packed (SGPR)
   int nout_full, nin_full, in_off, nin, nout, OT, KS;
 };
 
@@ -254,6 +254,21 @@ __global__ void k_prepare(PrepArgs a, float* __restrict__ wreg, int32_t* __restr
     const int64_t nW = (int64_t)g.nout_full * g.nin_full;
     for (int64_t i = threadIdx.x; i < nW + g.nout_full; i += blockDim.x)
       dst[i] = i < nW ? g.W[i] : g.b[i - nW];
+    return;
+  }
+  if (g.mode == 3) {  // W[nout][nin] (inputs from in_off) then b[nout], zero padded
+    const int64_t nW = (int64_t)g.nout * g.nin;
+    const int64_t n = (nW + g.nout + 15) & ~15;
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+      float v = 0.f;
+      if (i < nW) {
+        const int o = (int)(i / g.nin), k = (int)(i - (int64_t)o * g.nin);
+        v = g.W[(int64_t)o * g.nin_full + g.in_off + k];
+      } else if (i - nW < g.nout) {
+        v = g.b[i - nW];
+      }
+      dst[i] = v;
+    }
     return;
   }
   if (g.mode == 2) {
@@ -396,6 +411,19 @@ int prepare_run(const Shape& s, const float* const* params, void* prepared, hipS
       a.iq[j] = perm ? s.D - 1 - rev[j] : s.D - 1 - j;
     }
     hipLaunchKernelGGL(k_prepare, dim3(a.nseg + 1), dim3(256), 0, st, a, wreg, idx);
+    if (!tiled && s.sp_ok) {
+      // second copy of the layer in the packed SGPR layout (no index block)
+      PrepArgs b = a;
+      int64_t d2 = s.sp_region + (int64_t)l * s.sp_net_floats * s.nets;
+      for (int k = 0; k < b.nseg; ++k) {
+        PrepSeg& g = b.seg[k];
+        const int i = k % s.n_lin;
+        g.mode = 3;
+        g.nout = i == s.n_lin - 1 ? s.DT : g.nout_full;
+        g.dst = d2 + (k / s.n_lin) * s.sp_net_floats + s.sp_lin_off[i];
+      }
+      hipLaunchKernelGGL(k_prepare, dim3(b.nseg), dim3(256), 0, st, b, wreg, idx);
+    }
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) {
       set_hip_error(err);

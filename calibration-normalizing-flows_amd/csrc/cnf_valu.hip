@@ -29,6 +29,7 @@
 
 #include "cnf_internal.h"
 #include "cnf_valu_common.h"
+#include "cnf_valu_io.h"
 
 namespace cnf {
 namespace {
@@ -36,208 +37,18 @@ namespace {
 using namespace valu;
 
 
-// Block barrier for LDS hand-offs only: waits for this wave's LDS traffic,
-// not for its outstanding global loads/stores (a __syncthreads() would also
-// drain vmcnt, serialising the prefetch and the output stores).
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
-template <int ROWS>
-__device__ __forceinline__ void tile_load(float* __restrict__ sm, const float* __restrict__ src,
-                                          int n, bool vec) {
-  const int tid = threadIdx.x;
-  int done = 0;
-  if (vec) {
-    const int n4 = n >> 2;
-    const float4* s4 = reinterpret_cast<const float4*>(src);
-    float4* d4 = reinterpret_cast<float4*>(sm);
-    for (int i = tid; i < n4; i += ROWS) d4[i] = s4[i];
-    done = n4 << 2;
-  }
-  for (int i = done + tid; i < n; i += ROWS) sm[i] = src[i];
-}
-
-template <int ROWS>
-__device__ __forceinline__ void tile_store(float* __restrict__ dst, const float* __restrict__ sm,
-                                           int n, bool vec) {
-  const int tid = threadIdx.x;
-  int done = 0;
-  if (vec) {
-    const int n4 = n >> 2;
-    float4* d4 = reinterpret_cast<float4*>(dst);
-    const float4* s4 = reinterpret_cast<const float4*>(sm);
-    for (int i = tid; i < n4; i += ROWS) d4[i] = s4[i];
-    done = n4 << 2;
-  }
-  for (int i = done + tid; i < n; i += ROWS) dst[i] = sm[i];
-}
-
-// lane value <-> the RW rows a thread owns (rows tid and tid + ROWS of the tile)
-template <int ROWS>
-__device__ __forceinline__ float get_row(const float* sm, int i, int D, int k, float) {
-  return sm[i * D + k];
-}
-template <int ROWS, class V>
-__device__ __forceinline__ V get_row(const float* sm, int i, int D, int k, V) {
-  V r;
-#pragma unroll
-  for (int q = 0; q < (int)(sizeof(V) / sizeof(float)); ++q) r[q] = sm[(i + q * ROWS) * D + k];
-  return r;
-}
-template <int ROWS>
-__device__ __forceinline__ void put_row(float* sm, int i, int D, int k, float v) {
-  sm[i * D + k] = v;
-}
-template <int ROWS, class V>
-__device__ __forceinline__ void put_row(float* sm, int i, int D, int k, V v) {
-#pragma unroll
-  for (int q = 0; q < (int)(sizeof(V) / sizeof(float)); ++q) sm[(i + q * ROWS) * D + k] = v[q];
-}
-
-// Write the tile's rows (registers in orientation O) to dst through LDS.
-template <int D, int ROWS, bool O, class T>
-__device__ __forceinline__ void store_rows(float* __restrict__ dst, float* sm, const T* v,
-                                           int nrows, bool vec) {
-  const int tid = threadIdx.x;
-  lds_barrier();  // previous users of sm are done
-#pragma unroll
-  for (int j = 0; j < D; ++j) put_row<ROWS>(sm, tid, D, j, v[R<D, O>(j)]);
-  lds_barrier();
-  tile_store<ROWS>(dst, sm, nrows * D, vec);
-}
-
-__device__ __forceinline__ float comp(float v, int) { return v; }
-template <class V>
-__device__ __forceinline__ float comp(V v, int q) { return v[q]; }
-
-// Per-row terms of the calibrator loss on the final logits z (logical order):
-// CAL: loss = -(log(softmax(z)[y] + 1e-7) + ld)       calibrators.py:288-291
-// CE:  loss = -log_softmax(z)[y] - det * ld            run_experiment3D.py:107
-template <int D>
-__device__ __forceinline__ void row_loss(const float* z, float ld, int y, int kind, float det,
-                                         float& t0, float& t1, float& t2) {
-  float m = z[0];
-#pragma unroll
-  for (int j = 1; j < D; ++j) m = fmaxf(m, z[j]);
-  float se = 0.f, zy = z[0];
-#pragma unroll
-  for (int j = 0; j < D; ++j) {
-    se += __expf(z[j] - m);
-    zy = (j == y) ? opaque(z[j]) : zy;
-  }
-  const float lpy = zy - (m + __logf(se));
-  float ce, loss;
-  if (kind == CNF_LOSS_CAL) {
-    ce = -__logf(__expf(lpy) + 1e-7f);
-    loss = ce - ld;
-  } else {
-    ce = -lpy;
-    loss = ce - det * ld;
-  }
-  t0 += loss;
-  t1 += ce;
-  t2 += ld;
-}
-
-// Block sum of three per-thread values in a fixed order -> part[blockIdx]; the
-// block that arrives last (device-scope ticket) adds every block's partial in
-// block order and writes terms[0..2] -- deterministic, one launch.  Hand-off
-// per cdna_hip_programming.md Guideline 16, write-through form: the partials
-// are stored sc1 (agent-scope relaxed atomic stores), drained with vmcnt(0),
-// then a relaxed agent ticket add; the last arriver reads every partial with
-// sc1 loads.  No release fence: on this kernel it would write back the
-// whole XCD L2 (every block's freshly written z tile) once per block.  The
-// last arriver resets the ticket for the next call (the workspace starts
-// zeroed).
-template <int ROWS>
-__device__ __forceinline__ void block_sum3(float a, float b, float c, float* sm, float* part,
-                                           unsigned* ticket, float* terms, int nblk) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    a += __shfl_xor(a, off);
-    b += __shfl_xor(b, off);
-    c += __shfl_xor(c, off);
-  }
-  const int tid = threadIdx.x, w = tid >> 6;
-  lds_barrier();
-  if ((tid & 63) == 0) {
-    sm[4 * w] = a;
-    sm[4 * w + 1] = b;
-    sm[4 * w + 2] = c;
-  }
-  lds_barrier();
-  if (tid == 0) {
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
-    for (int i = 0; i < ROWS / 64; ++i) {
-      s0 += sm[4 * i];
-      s1 += sm[4 * i + 1];
-      s2 += sm[4 * i + 2];
-    }
-    float* dst = part + (int64_t)blockIdx.x * 4;
-    __hip_atomic_store(dst, s0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(dst + 1, s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(dst + 2, s2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT);
-    sm[64] = t == (unsigned)(nblk - 1) ? 1.f : 0.f;
-  }
-  __syncthreads();
-  if (sm[64] == 0.f) return;  // block-uniform
-  float r0 = 0.f, r1 = 0.f, r2 = 0.f;
-  for (int bb = tid; bb < nblk; bb += ROWS) {
-    const float* src = part + (int64_t)bb * 4;
-    r0 += __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    r1 += __hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    r2 += __hip_atomic_load(src + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  sm[tid] = r0;
-  sm[ROWS + tid] = r1;
-  sm[2 * ROWS + tid] = r2;
-  __syncthreads();
-  for (int h = ROWS / 2; h >= 1; h >>= 1) {
-    if (tid < h) {
-      sm[tid] += sm[tid + h];
-      sm[ROWS + tid] += sm[ROWS + tid + h];
-      sm[2 * ROWS + tid] += sm[2 * ROWS + tid + h];
-    }
-    __syncthreads();
-  }
-  if (tid == 0) {
-    terms[0] = sm[0];
-    terms[1] = sm[ROWS];
-    terms[2] = sm[2 * ROWS];
-    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-template <int ROWS>
-__device__ __forceinline__ void store_ld(float* ld_out, int64_t row0, int tid, int nrows, float v) {
-  if (tid < nrows) ld_out[row0 + tid] = v;
-}
-template <int ROWS, class V>
-__device__ __forceinline__ void store_ld(float* ld_out, int64_t row0, int tid, int nrows, V v) {
-#pragma unroll
-  for (int q = 0; q < (int)(sizeof(V) / sizeof(float)); ++q)
-    if (tid + q * ROWS < nrows) ld_out[row0 + tid + q * ROWS] = v[q];
-}
-
 // Fused L-layer coupling pass.  One block = ROWS threads = ROWS*RW logit
 // vectors per tile.  PERSIST: a grid of (CUs x resident blocks) walks the
 // tiles, prefetching the next tile's input into registers (16-B loads) while
 // the current tile computes.
 template <int D, int H1, int H2, bool INV, bool STRICT, int RW, int ROWS, bool PERSIST, int WPE,
-          bool FX, bool WL, bool WU = false, bool CH = false>
+          bool FX, bool WL, bool WU = false, bool CH = false, bool DUP = false>
 __global__ __launch_bounds__(ROWS, WPE) void k_valu(
     const float* __restrict__ Wg, const int32_t* __restrict__ qtab,
     const int32_t* __restrict__ lflag, const float* __restrict__ in, float* __restrict__ out,
     float* __restrict__ ld_out, float* __restrict__ all, int64_t B, int L, int scale, int shift,
     int any_perm, int vec_io, const int64_t* __restrict__ yl, float* __restrict__ loss_part,
-    int kind, float det, unsigned* __restrict__ ticket, float* __restrict__ loss_terms) {
+    int kind, float det, unsigned*, float*) {
   using T = typename RowT<RW>::type;
   constexpr int TR = ROWS * RW;  // rows per tile
   constexpr int TF = TR * D;     // floats per tile
@@ -256,10 +67,21 @@ __global__ __launch_bounds__(ROWS, WPE) void k_valu(
     const int n4 = (L * layer_floats) >> 2;  // layer_floats % 4 == 0 (compact layout)
     const float4* s4 = reinterpret_cast<const float4*>(Wg);
     float4* d4 = reinterpret_cast<float4*>(wl);
-    for (int i = tid; i < n4; i += ROWS) d4[i] = s4[i];
+    if constexpr (DUP) {
+      // each weight twice: the pair is the packed operand for the RW=2 rows
+      for (int i = tid; i < n4; i += ROWS) {
+        const float4 a = s4[i];
+        d4[2 * i] = float4{a.x, a.x, a.y, a.y};
+        d4[2 * i + 1] = float4{a.z, a.z, a.w, a.w};
+      }
+    } else {
+      for (int i = tid; i < n4; i += ROWS) d4[i] = s4[i];
+    }
     lds_barrier();
     W = wl;
   }
+  using WP = typename std::conditional<DUP, f2, float>::type;
+  const WP* WW = reinterpret_cast<const WP*>(W);
   const int64_t ntiles = (B + TR - 1) / TR;
   const int64_t nfull = B / TR;  // tiles whose TF floats are all in range
   const int64_t stride = PERSIST ? (int64_t)gridDim.x : ntiles;
@@ -310,6 +132,8 @@ __global__ __launch_bounds__(ROWS, WPE) void k_valu(
     } else {
       tile_load<ROWS>(sm, in + row0 * D, nrows * D, vec);
     }
+    int yv[RW];
+    if (loss_part) load_labels<RW>(yl, row0, tid, ROWS, B, yv);
     lds_barrier();
     if constexpr (PERSIST) {
       const int64_t nt = tile + stride;
@@ -331,10 +155,10 @@ __global__ __launch_bounds__(ROWS, WPE) void k_valu(
     for (; i + 1 < L; i += 2) {
       int la = layer_of(i), lb = layer_of(i + 1);
       bool pa = any_perm && (lflag[la] & kFlagPerm), pb = any_perm && (lflag[lb] & kFlagPerm);
-      step<D, H1, H2, INV, STRICT, false, FX && !STRICT, CH && !WL>(v, ld, W + (int64_t)la * layer_floats, scale, shift,
+      step<D, H1, H2, INV, STRICT, false, FX && !STRICT, CH && !WL>(v, ld, WW + (int64_t)la * layer_floats, scale, shift,
                                           NF, pa, qtab + la * D);
       if (all) store_rows<D, ROWS, true>(all + (int64_t)i * B * D + row0 * D, sm, v, nrows, vec);
-      step<D, H1, H2, INV, STRICT, true, FX && !STRICT, CH && !WL>(v, ld, W + (int64_t)lb * layer_floats, scale, shift,
+      step<D, H1, H2, INV, STRICT, true, FX && !STRICT, CH && !WL>(v, ld, WW + (int64_t)lb * layer_floats, scale, shift,
                                          NF, pb, qtab + lb * D);
       if (all)
         store_rows<D, ROWS, false>(all + (int64_t)(i + 1) * B * D + row0 * D, sm, v, nrows, vec);
@@ -343,7 +167,7 @@ __global__ __launch_bounds__(ROWS, WPE) void k_valu(
     if (odd) {
       int la = layer_of(i);
       bool pa = any_perm && (lflag[la] & kFlagPerm);
-      step<D, H1, H2, INV, STRICT, false, FX && !STRICT, CH && !WL>(v, ld, W + (int64_t)la * layer_floats, scale, shift,
+      step<D, H1, H2, INV, STRICT, false, FX && !STRICT, CH && !WL>(v, ld, WW + (int64_t)la * layer_floats, scale, shift,
                                           NF, pa, qtab + la * D);
       if (all) store_rows<D, ROWS, true>(all + (int64_t)i * B * D + row0 * D, sm, v, nrows, vec);
     }
@@ -353,19 +177,11 @@ __global__ __launch_bounds__(ROWS, WPE) void k_valu(
     }
     if (ld_out) store_ld<ROWS>(ld_out, row0, tid, nrows, ld);
     if (loss_part) {
-#pragma unroll
-      for (int q = 0; q < RW; ++q) {
-        const int64_t row = row0 + tid + q * ROWS;
-        if (row < B) {
-          float z[D];
-#pragma unroll
-          for (int j = 0; j < D; ++j) z[j] = odd ? comp(v[D - 1 - j], q) : comp(v[j], q);
-          row_loss<D>(z, comp(ld, q), (int)yl[row], kind, det, lt0, lt1, lt2);
-        }
-      }
+      if (odd) tile_loss<D, true>(v, ld, yv, kind, det, lt0, lt1, lt2);
+      else tile_loss<D, false>(v, ld, yv, kind, det, lt0, lt1, lt2);
     }
   }
-  if (loss_part) block_sum3<ROWS>(lt0, lt1, lt2, smem, loss_part, ticket, loss_terms, gridDim.x);
+  if (loss_part) block_sum3<ROWS>(lt0, lt1, lt2, smem, loss_part);
 }
 
 // ---------------------------------------------------------------------------
@@ -377,15 +193,17 @@ using KFn = void (*)(const float*, const int32_t*, const int32_t*, const float*,
 
 struct Variant {
   KFn fn[2][2];  // [inverse][strict]
-  int rw, rows, persist, wl;
+  int rw, rows, persist, wl;  // wl: 0 scalar weights, 1 LDS, 2 LDS pairs (DUP)
 };
 
-#define CNF_VARIANT_X(D, H1, H2, RW, ROWS, P, WPE, FX, WL, WU, CH)                        \
-  {{{k_valu<D, H1, H2, false, false, RW, ROWS, P, WPE, FX, WL, WU, CH>,                    \
-     k_valu<D, H1, H2, false, true, RW, ROWS, P, WPE, FX, WL, WU, CH>},                    \
-    {k_valu<D, H1, H2, true, false, RW, ROWS, P, WPE, FX, WL, WU, CH>,                     \
-     k_valu<D, H1, H2, true, true, RW, ROWS, P, WPE, FX, WL, WU, CH>}},                    \
-   RW, ROWS, P, WL}
+#define CNF_VARIANT_Y(D, H1, H2, RW, ROWS, P, WPE, FX, WL, WU, CH, DUP)                        \
+  {{{k_valu<D, H1, H2, false, false, RW, ROWS, P, WPE, FX, WL, WU, CH, DUP>,                    \
+     k_valu<D, H1, H2, false, true, RW, ROWS, P, WPE, FX, WL, WU, CH, DUP>},                    \
+    {k_valu<D, H1, H2, true, false, RW, ROWS, P, WPE, FX, WL, WU, CH, DUP>,                     \
+     k_valu<D, H1, H2, true, true, RW, ROWS, P, WPE, FX, WL, WU, CH, DUP>}},                    \
+   RW, ROWS, P, (WL) ? ((DUP) ? 2 : 1) : 0}
+#define CNF_VARIANT_X(D, H1, H2, RW, ROWS, P, WPE, FX, WL, WU, CH) \
+  CNF_VARIANT_Y(D, H1, H2, RW, ROWS, P, WPE, FX, WL, WU, CH, false)
 #define CNF_VARIANT_U(D, H1, H2, RW, ROWS, P, WPE, FX, WL, WU) \
   CNF_VARIANT_X(D, H1, H2, RW, ROWS, P, WPE, FX, WL, WU, false)
 #define CNF_VARIANT(D, H1, H2, RW, ROWS, P, WPE, FX, WL) \
@@ -433,6 +251,7 @@ const Variant kExp[] = {
     CNF_VARIANT(10, 5, 5, 2, 256, false, 4, true, false),                 // 5: scalar, 2/lane
     CNF_VARIANT(10, 5, 5, 2, 128, false, 4, true, true),                  // 6: LDS, 2/lane, 128 thr
     CNF_VARIANT(10, 5, 5, 1, 256, false, 6, true, true),                  // 7: LDS, 1/lane
+    CNF_VARIANT_Y(10, 5, 5, 2, 256, false, 4, true, true, false, false, true),  // 8: LDS pairs
 };
 
 int cu_count() {
@@ -495,6 +314,7 @@ static int64_t blocks_for(const Shape& s, const Variant* var, KFn fn, int64_t B)
 
 int valu_loss_blocks(const Shape& s, int64_t B) {
   if (s.valu_id < 0) return -1;
+  if (sgpr_enabled(s)) return (int)sgpr_blocks(B);
   const Variant* var = pick_variant(s, B);
   return (int)blocks_for(s, var, var->fn[0][s.strict ? 1 : 0], B);
 }
@@ -504,6 +324,9 @@ int valu_run(const Shape& s, const void* prepared, const float* in, float* out, 
              float* loss_ws, int kind, float det, float* loss_terms) {
   if (s.valu_id < 0) return CNF_ERR_UNSUPPORTED;
   if (B == 0) return CNF_OK;
+  if (sgpr_enabled(s) && !all)
+    return sgpr_run(s, prepared, in, out, ld, all, B, inverse, st, y, loss_ws, kind, det,
+                    loss_terms);
   const Entry& e = kTable[s.valu_id];
   if (e.nf != s.valu_net_floats) return CNF_ERR_DESC;  // host/device layout disagree
   const Variant* var = pick_variant(s, B);
@@ -519,12 +342,13 @@ int valu_run(const Shape& s, const void* prepared, const float* in, float* out, 
   const int64_t nblk = blocks_for(s, var, fn, B);
   size_t lds = (size_t)tr * s.D * 4;
   if (lds < (size_t)3 * var->rows * 4 + 4 * 65) lds = (size_t)3 * var->rows * 4 + 4 * 65;
-  if (var->wl) lds += (size_t)s.L * s.nets * s.valu_net_floats * 4;
+  if (var->wl) lds += (size_t)s.L * s.nets * s.valu_net_floats * 4 * var->wl;
   if (lds > 160 * 1024) return CNF_ERR_UNSUPPORTED;
   hipLaunchKernelGGL(fn, dim3((unsigned)nblk), dim3(var->rows), lds, st, W,
                      inverse ? inv_q : fwd_q, flags, in, out, ld, all, B, s.L, s.scale, s.shift,
                      s.any_perm ? 1 : 0, vec, y, loss_ws ? loss_ws + 4 : nullptr, kind, det,
-                     reinterpret_cast<unsigned*>(loss_ws), loss_terms);
+                     nullptr, nullptr);
+  if (loss_ws) reduce_partials(loss_ws + 4, (int)nblk, 4, 0, nullptr, loss_terms, st);
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) {
     set_hip_error(err);

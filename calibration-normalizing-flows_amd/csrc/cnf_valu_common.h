@@ -25,9 +25,25 @@ template <> struct RowT<4> { typedef f4 type; };
 __device__ __forceinline__ float splat(float w, float) { return w; }
 template <class V>
 __device__ __forceinline__ V splat(float w, V) { return V(w); }
+__device__ __forceinline__ float maxT(float a, float b) { return fmaxf(a, b); }
+template <class V>
+__device__ __forceinline__ V maxT(V a, V b) { return __builtin_elementwise_max(a, b); }
+__device__ __forceinline__ float exp2T(float x) { return __builtin_amdgcn_exp2f(x); }
+template <class V>
+__device__ __forceinline__ V exp2T(V x) {
+  V r;
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(V) / sizeof(float)); ++i) r[i] = __builtin_amdgcn_exp2f(x[i]);
+  return r;
+}
+__device__ __forceinline__ void setc(float& v, int, float x) { v = x; }
+template <class V>
+__device__ __forceinline__ void setc(V& v, int q, float x) { v[q] = x; }
 __device__ __forceinline__ float fmaT(float w, float x, float a) { return fmaf(w, x, a); }
 template <class V>
 __device__ __forceinline__ V fmaT(float w, V x, V a) { return __builtin_elementwise_fma(V(w), x, a); }
+__device__ __forceinline__ f2 fmaT(f2 w, f2 x, f2 a) { return __builtin_elementwise_fma(w, x, a); }
+__device__ __forceinline__ f2 splat(f2 w, f2) { return w; }
 __device__ __forceinline__ float fmaV(float x, float y, float a) { return fmaf(x, y, a); }
 template <class V>
 __device__ __forceinline__ V fmaV(V x, V y, V a) { return __builtin_elementwise_fma(x, y, a); }
@@ -82,6 +98,12 @@ __device__ __forceinline__ float wget(const float* __restrict__ w, int i) {
   return reinterpret_cast<const v16f*>(w)[i >> 4][i & 15];
 }
 
+// Weight i of a Linear block: float blobs read as wide scalar chunks; pair
+// blobs (each weight stored twice, LDS) read as one 8-B element that is
+// directly the packed operand of v_pk_fma_f32 for two vectors per lane.
+__device__ __forceinline__ float wld(const float* __restrict__ w, int i) { return wget(w, i); }
+__device__ __forceinline__ f2 wld(const f2* __restrict__ w, int i) { return w[i]; }
+
 template <int D, int H1, int H2>
 struct Net {
   static constexpr int DT = D / 2, DC = D - D / 2;
@@ -92,15 +114,15 @@ struct Net {
 };
 
 // y[o] = b[o] (+p0) + sum_k W[o][k] * x[k],  o < NOUT <= NOUTF.
-template <int NIN, int NOUTF, int NOUT, bool RELU, bool STRICT, bool POISON, class T>
-__device__ __forceinline__ void linear(const float* __restrict__ w, const T* x, T* y, T p0) {
+template <int NIN, int NOUTF, int NOUT, bool RELU, bool STRICT, bool POISON, class T, class WP>
+__device__ __forceinline__ void linear(const WP* __restrict__ w, const T* x, T* y, T p0) {
   constexpr int S = Lin<NIN, NOUTF>::stride;
 #pragma unroll
   for (int o = 0; o < NOUT; ++o) {
 #ifdef CNF_DIAG_FAKE_WEIGHTS
     T a = splat(0.001f * o, T{});
 #else
-    T a = splat(wget(w, NOUTF * S + o), T{});
+    T a = splat(wld(w, NOUTF * S + o), T{});
 #endif
     if constexpr (POISON) a += p0;
 #pragma unroll
@@ -108,7 +130,7 @@ __device__ __forceinline__ void linear(const float* __restrict__ w, const T* x, 
 #ifdef CNF_DIAG_FAKE_WEIGHTS  // diagnostic build only: weights as literals (no loads)
       a = fmaT(0.01f * (float)(o * 7 + k + 1) + 1e-4f * S, x[k], a);
 #else
-      a = fmaT(wget(w, o * S + k), x[k], a);
+      a = fmaT(wld(w, o * S + k), x[k], a);
 #endif
     }
     y[o] = RELU ? relu<STRICT>(a) : a;
@@ -161,17 +183,18 @@ __device__ __forceinline__ void linear_chunked(const float* __restrict__ w, cons
 }
 
 // Linear through the chunked scalar path when the block fits 3 chunks.
-template <int NIN, int NOUTF, int NOUT, bool RELU, bool STRICT, bool POISON, bool CH, class T>
-__device__ __forceinline__ void linear_any(const float* __restrict__ w, const T* x, T* y, T p0) {
-  if constexpr (CH && Lin<NIN, NOUTF>::floats <= 48)
+template <int NIN, int NOUTF, int NOUT, bool RELU, bool STRICT, bool POISON, bool CH, class T,
+          class WP>
+__device__ __forceinline__ void linear_any(const WP* __restrict__ w, const T* x, T* y, T p0) {
+  if constexpr (CH && sizeof(WP) == 4 && Lin<NIN, NOUTF>::floats <= 48)
     linear_chunked<NIN, NOUTF, NOUT, RELU, STRICT, POISON>(w, x, y, p0);
   else
     linear<NIN, NOUTF, NOUT, RELU, STRICT, POISON>(w, x, y, p0);
 }
 
 // Conditioner MLP on the conditioning half c[DC].
-template <int D, int H1, int H2, int NO, bool STRICT, bool CH = false, class T>
-__device__ __forceinline__ void mlp(const float* __restrict__ w, const T* c, T p0, T* o) {
+template <int D, int H1, int H2, int NO, bool STRICT, bool CH = false, class T, class WP>
+__device__ __forceinline__ void mlp(const WP* __restrict__ w, const T* c, T p0, T* o) {
   constexpr int DC = D - D / 2;
   const T z = splat(0.f, T{});
   if constexpr (H1 == 0) {
@@ -183,7 +206,7 @@ __device__ __forceinline__ void mlp(const float* __restrict__ w, const T* c, T p
   } else {
     T h1[H1], h2[H2];
     linear_any<DC, H1, H1, true, STRICT, STRICT, CH>(w, c, h1, p0);
-    const float* w2 = w + Lin<DC, H1>::floats;
+    const WP* w2 = w + Lin<DC, H1>::floats;
     linear_any<H1, H2, H2, true, STRICT, false, CH>(w2, h1, h2, z);
     linear_any<H2, D, NO, false, STRICT, false, CH>(w2 + Lin<H1, H2>::floats, h2, o, z);
   }
@@ -223,8 +246,9 @@ __device__ __forceinline__ void permute(T* v, const int32_t* __restrict__ q) {
 }
 
 // One coupling layer, input in orientation O, output in orientation !O.
-template <int D, int H1, int H2, bool INV, bool STRICT, bool O, bool FX, bool CH, class T>
-__device__ __forceinline__ void step(T* v, T& ld, const float* __restrict__ wl, int scale,
+template <int D, int H1, int H2, bool INV, bool STRICT, bool O, bool FX, bool CH, class T,
+          class WP>
+__device__ __forceinline__ void step(T* v, T& ld, const WP* __restrict__ wl, int scale,
                                      int shift, int net_floats, bool perm,
                                      const int32_t* __restrict__ q) {
   constexpr int DT = D / 2, DC = D - D / 2;

@@ -1,0 +1,192 @@
+// Tile I/O and loss helpers shared by the narrow-flow forward kernels
+// (cnf_valu.hip: LDS / scalar weights; cnf_sgpr.hip: pipelined scalar weights).
+// A block owns a tile of ROWS*RW rows staged through LDS, so global loads and
+// stores are 16-byte-per-lane coalesced sweeps; a lane holds RW rows.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "cnf_valu_common.h"
+
+namespace cnf {
+namespace valu {
+
+// Block barrier for LDS hand-offs only: waits for this wave's LDS traffic,
+// not for its outstanding global loads/stores (a __syncthreads() would also
+// drain vmcnt, serialising the prefetch and the output stores).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int ROWS>
+__device__ __forceinline__ void tile_load(float* __restrict__ sm, const float* __restrict__ src,
+                                          int n, bool vec) {
+  const int tid = threadIdx.x;
+  int done = 0;
+  if (vec) {
+    const int n4 = n >> 2;
+    const float4* s4 = reinterpret_cast<const float4*>(src);
+    float4* d4 = reinterpret_cast<float4*>(sm);
+    for (int i = tid; i < n4; i += ROWS) d4[i] = s4[i];
+    done = n4 << 2;
+  }
+  for (int i = done + tid; i < n; i += ROWS) sm[i] = src[i];
+}
+
+template <int ROWS>
+__device__ __forceinline__ void tile_store(float* __restrict__ dst, const float* __restrict__ sm,
+                                           int n, bool vec) {
+  const int tid = threadIdx.x;
+  int done = 0;
+  if (vec) {
+    const int n4 = n >> 2;
+    float4* d4 = reinterpret_cast<float4*>(dst);
+    const float4* s4 = reinterpret_cast<const float4*>(sm);
+    for (int i = tid; i < n4; i += ROWS) d4[i] = s4[i];
+    done = n4 << 2;
+  }
+  for (int i = done + tid; i < n; i += ROWS) dst[i] = sm[i];
+}
+
+// lane value <-> the RW rows a thread owns (rows tid and tid + ROWS of the tile)
+template <int ROWS>
+__device__ __forceinline__ float get_row(const float* sm, int i, int D, int k, float) {
+  return sm[i * D + k];
+}
+template <int ROWS, class V>
+__device__ __forceinline__ V get_row(const float* sm, int i, int D, int k, V) {
+  V r;
+#pragma unroll
+  for (int q = 0; q < (int)(sizeof(V) / sizeof(float)); ++q) r[q] = sm[(i + q * ROWS) * D + k];
+  return r;
+}
+template <int ROWS>
+__device__ __forceinline__ void put_row(float* sm, int i, int D, int k, float v) {
+  sm[i * D + k] = v;
+}
+template <int ROWS, class V>
+__device__ __forceinline__ void put_row(float* sm, int i, int D, int k, V v) {
+#pragma unroll
+  for (int q = 0; q < (int)(sizeof(V) / sizeof(float)); ++q) sm[(i + q * ROWS) * D + k] = v[q];
+}
+
+// Write the tile's rows (registers in orientation O) to dst through LDS.
+template <int D, int ROWS, bool O, class T>
+__device__ __forceinline__ void store_rows(float* __restrict__ dst, float* sm, const T* v,
+                                           int nrows, bool vec) {
+  const int tid = threadIdx.x;
+  lds_barrier();  // previous users of sm are done
+#pragma unroll
+  for (int j = 0; j < D; ++j) put_row<ROWS>(sm, tid, D, j, v[R<D, O>(j)]);
+  lds_barrier();
+  tile_store<ROWS>(dst, sm, nrows * D, vec);
+}
+
+__device__ __forceinline__ float comp(float v, int) { return v; }
+template <class V>
+__device__ __forceinline__ float comp(V v, int q) { return v[q]; }
+
+// Loss terms of the tile's rows (registers in orientation O, RW rows per lane):
+// CAL: loss = -(log(softmax(z)[y] + 1e-7) + ld)       calibrators.py:288-291
+// CE:  loss = -log_softmax(z)[y] - det * ld            run_experiment3D.py:107
+// The max / shifted-exp / sum run on whole RW-row vectors (packed FMAs);
+// z[y] is a sum of per-lane selects (a select chain over an array would be
+// folded into a dynamically indexed scratch load).
+// Labels of the lane's RW rows (low 32-bit word of the int64 targets; -1 past
+// the batch end), issued with the tile load so the latency hides under the
+// layer sweep instead of stalling the loss at the end.
+template <int RW>
+__device__ __forceinline__ void load_labels(const int64_t* __restrict__ yl, int64_t row0, int tid,
+                                            int rows, int64_t B, int* y) {
+  const int32_t* y32 = reinterpret_cast<const int32_t*>(yl);
+#pragma unroll
+  for (int q = 0; q < RW; ++q) {
+    const int64_t row = row0 + tid + (int64_t)q * rows;
+    y[q] = row < B ? y32[2 * row] : -1;
+  }
+}
+
+template <int D, bool O, class T>
+__device__ __forceinline__ void tile_loss(const T* v, T ld, const int* y, int kind, float det,
+                                          float& t0, float& t1, float& t2) {
+  constexpr int RW = sizeof(T) / sizeof(float);
+  constexpr float kL2E = 1.4426950408889634f, kLN2 = 0.6931471805599453f;
+  T m = v[R<D, O>(0)];
+#pragma unroll
+  for (int j = 1; j < D; ++j) m = maxT(m, v[R<D, O>(j)]);
+  const T nm = m * splat(-kL2E, T{});
+  T se = splat(0.f, T{}), zy = splat(0.f, T{});
+#pragma unroll
+  for (int j = 0; j < D; ++j) {
+    const T zj = v[R<D, O>(j)];
+    se += exp2T(fmaT(kL2E, zj, nm));
+#pragma unroll
+    for (int q = 0; q < RW; ++q) setc(zy, q, comp(zy, q) + (j == y[q] ? comp(zj, q) : 0.f));
+  }
+#pragma unroll
+  for (int q = 0; q < RW; ++q) {
+    if (y[q] < 0) continue;
+    const float lpy = comp(zy, q) - (comp(m, q) + __builtin_amdgcn_logf(comp(se, q)) * kLN2);
+    const float l = comp(ld, q);
+    float ce, loss;
+    if (kind == CNF_LOSS_CAL) {
+      ce = -__builtin_amdgcn_logf(__builtin_amdgcn_exp2f(lpy * kL2E) + 1e-7f) * kLN2;
+      loss = ce - l;
+    } else {
+      ce = -lpy;
+      loss = ce - det * l;
+    }
+    t0 += loss;
+    t1 += ce;
+    t2 += l;
+  }
+}
+
+// Block sum of three per-thread values in a fixed order -> part[blockIdx][0..2]
+// (plain stores; the wave exits right after).  The host side adds the
+// partials in block order with one small follow-up launch (reduce_partials),
+// so the fused eval stays deterministic without any block waiting on a
+// device-scope hand-off.
+template <int ROWS>
+__device__ __forceinline__ void block_sum3(float a, float b, float c, float* sm, float* part) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    a += __shfl_xor(a, off);
+    b += __shfl_xor(b, off);
+    c += __shfl_xor(c, off);
+  }
+  const int tid = threadIdx.x, w = tid >> 6;
+  lds_barrier();
+  if ((tid & 63) == 0) {
+    sm[4 * w] = a;
+    sm[4 * w + 1] = b;
+    sm[4 * w + 2] = c;
+  }
+  lds_barrier();
+  if (tid == 0) {
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+    for (int i = 0; i < ROWS / 64; ++i) {
+      s0 += sm[4 * i];
+      s1 += sm[4 * i + 1];
+      s2 += sm[4 * i + 2];
+    }
+    reinterpret_cast<float4*>(part)[blockIdx.x] = float4{s0, s1, s2, 0.f};
+  }
+}
+
+template <int ROWS>
+__device__ __forceinline__ void store_ld(float* ld_out, int64_t row0, int tid, int nrows, float v) {
+  if (tid < nrows) ld_out[row0 + tid] = v;
+}
+template <int ROWS, class V>
+__device__ __forceinline__ void store_ld(float* ld_out, int64_t row0, int tid, int nrows, V v) {
+#pragma unroll
+  for (int q = 0; q < (int)(sizeof(V) / sizeof(float)); ++q)
+    if (tid + q * ROWS < nrows) ld_out[row0 + tid + q * ROWS] = v[q];
+}
+
+}  // namespace valu
+}  // namespace cnf

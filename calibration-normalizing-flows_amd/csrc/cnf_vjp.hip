@@ -446,15 +446,30 @@ __global__ __launch_bounds__(256) void k_reduce_cols(const float* __restrict__ p
                                   red[threadIdx.x + 128]) + red[threadIdx.x + 192];
 }
 
-// Few entries (the 3 loss sums): one block, thread t adds blocks t, t+256, ...
-// then a fixed LDS tree.
-__global__ __launch_bounds__(256) void k_reduce_rows(const float* __restrict__ partials,
-                                                     int nblk, int PS, int E0, int NE,
-                                                     float* __restrict__ out) {
-  __shared__ float red[4][256];
+// Few entries (the 3 loss sums): one 1024-thread block; thread t adds blocks
+// t, t+1024, ... in order (four independent loads in flight per entry), then
+// a fixed LDS tree -- deterministic for a given nblk.
+__global__ __launch_bounds__(1024) void k_reduce_rows(const float* __restrict__ partials,
+                                                      int nblk, int PS, int E0, int NE,
+                                                      float* __restrict__ out) {
+  constexpr int T = 1024;
+  __shared__ float red[4][T];
   const int t = threadIdx.x;
   float s[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int b = t; b < nblk; b += 256) {
+  int b = t;
+  for (; b + 3 * T < nblk; b += 4 * T) {
+    float v[4][4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        v[k][e] = e < NE ? partials[(int64_t)(b + k * T) * PS + E0 + e] : 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s[e] += v[k][e];
+  }
+  for (; b < nblk; b += T) {
 #pragma unroll
     for (int e = 0; e < 4; ++e)
       if (e < NE) s[e] += partials[(int64_t)b * PS + E0 + e];
@@ -462,7 +477,7 @@ __global__ __launch_bounds__(256) void k_reduce_rows(const float* __restrict__ p
 #pragma unroll
   for (int e = 0; e < 4; ++e) red[e][t] = s[e];
   __syncthreads();
-  for (int w = 128; w >= 1; w >>= 1) {
+  for (int w = T / 2; w >= 1; w >>= 1) {
     if (t < w) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) red[e][t] += red[e][t + w];
@@ -521,7 +536,7 @@ int reduce_partials(const float* partials, int nblk, int PS, int P, float* grads
     hipLaunchKernelGGL(k_reduce_cols, dim3((unsigned)((P + 63) / 64)), dim3(256), 0, st,
                        partials, nblk, PS, P, grads);
   if (terms)
-    hipLaunchKernelGGL(k_reduce_rows, dim3(1), dim3(256), 0, st, partials, nblk, PS, P, 3,
+    hipLaunchKernelGGL(k_reduce_rows, dim3(1), dim3(1024), 0, st, partials, nblk, PS, P, 3,
                        terms);
   return CNF_OK;
 }

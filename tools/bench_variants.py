@@ -27,10 +27,18 @@ def main():
         if only and name not in only.split(","):
             continue
         r = bench.Runner(dict(wl), dev, 1.5e9, all_outputs=allo, mode=mode)
+        if mode == "loss":  # the partials area depends on the variant's grid
+            r.ws_bytes = 16 + 16 * (wl["B"] // 64 + 1)
+            r.ws = torch.zeros(r.ws_bytes, dtype=torch.uint8, device=dev)
         res = {v: [] for v in VARIANTS}
         for rnd in range(5):
             for v in VARIANTS:
-                os.environ["CNF_VALU_VARIANT"] = str(v)
+                if v == 99:  # pipelined-scalar kernel (cnf_sgpr.hip)
+                    os.environ["CNF_SGPR"] = "1"
+                    os.environ.pop("CNF_VALU_VARIANT", None)
+                else:
+                    os.environ["CNF_SGPR"] = "0"
+                    os.environ["CNF_VALU_VARIANT"] = str(v)
                 res[v].append(bench.kernel_only_seconds(r, 40))
         for v in VARIANTS:
             t = float(np.median(res[v]))
