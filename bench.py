@@ -127,6 +127,10 @@ class Runner:
             self.ws_bytes = n.value
         self.i = 0
 
+    def kernel_symbol(self):
+        return {"valu-fused": "k_valu", "sgpr-fused": "k_sgpr", "mfma-tile": "k_tile"}.get(
+            self.stack.kernel_name(), self.stack.kernel_name())
+
     def step(self):
         a = self.args[self.i % self.nsets]
         self.i += 1
@@ -198,6 +202,24 @@ def train_step_rate(dev, B=1 << 20, steps=20):
     t = e0.elapsed_time(e1) / 1e3 / steps
     return {"vec_per_s": round(B / t, 1), "ms_per_step": round(t * 1e3, 4), "B": B,
             "note": "forward + calibrator loss + VJP + gradient reduction; optimizer excluded"}
+
+
+def measured_traffic(workload, B):
+    """HBM bytes per launch of the bench kernel from the committed PMC summary
+    (profiles/<round>_traffic_<workload>.json, written by tools/pmc_traffic.py
+    from rocprofv3 FETCH_SIZE / WRITE_SIZE passes, gfx950-corrected), or None."""
+    import glob
+    best = None
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic_%s.json" % workload))):
+        try:
+            with open(p) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if int(d.get("B", -1)) == B:
+            d["source"] = "profiles/" + os.path.basename(p)
+            best = d
+    return best
 
 
 def cpu_baseline(w, seconds=10.0):
@@ -281,13 +303,18 @@ def main():
         "frac": None, "traffic": None,
         "kernel": runner.stack.kernel_name(),
         "kernel_avg_us": round(k_avg * 1e6, 3),
-        "timed_kernels": "k_valu (fused pass) + k_reduce (fixed-order NLL sum)" if mode == "loss"
-                         else "k_valu",
+        "timed_kernels": ("%s + k_reduce_rows (block-order NLL sum): the whole cnf_forward_loss "
+                          "call, HIP events on its stream" % runner.kernel_symbol()) if mode == "loss"
+                         else runner.kernel_symbol(),
         "algo_bytes_per_vec": bytes_vec, "algo_flops_per_vec": flops_vec,
         "valu_tflops": round(achieved_tf, 2), "valu_frac": round(achieved_tf / VALU_PEAK_TFLOPS, 4),
         "rotating_sets": runner.nsets,
     }
     roof["frac"] = round(roof["achieved"] / roof["peak"], 4)
+    tr = measured_traffic(args.workload, w["B"])
+    if tr is not None:
+        roof["traffic"] = tr["traffic_bytes_per_launch"]
+        roof["traffic_source"] = tr["source"]
 
     variants = {}
     if rank == 0 and world == 1 and not args.no_variants:

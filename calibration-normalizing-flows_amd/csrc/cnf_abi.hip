@@ -70,7 +70,7 @@ int derive_shape(const cnf_desc* d, Shape* s) {
     for (int i = 0; i < s->n_lin; ++i) {
       const int nin = i == 0 ? s->DC : s->units[i];
       const int nout = i == s->n_lin - 1 ? s->DT : s->units[i + 1];
-      const int64_t f = ((int64_t)nout * nin + nout + 15) & ~15;
+      const int64_t f = ((int64_t)nout * ((nin + 2) & ~1) + 15) & ~15;  // cnf_sgpr.hip SP
       if (f > 32) s->sp_ok = false;
       s->sp_lin_off[i] = off;
       off += f;
@@ -260,7 +260,8 @@ int cnf_loss_vjp(const cnf_desc* desc, const void* prepared, const float* x, con
 const char* cnf_kernel_name(const cnf_desc* desc) {
   Shape s;
   if (derive_shape(desc, &s) != CNF_OK) return "unsupported";
-  return s.family == Family::kValu ? "valu-fused" : "mfma-tile";
+  if (s.family != Family::kValu) return "mfma-tile";
+  return sgpr_enabled(s) ? "sgpr-fused" : "valu-fused";
 }
 
 }  // extern "C"

@@ -71,7 +71,7 @@ int valu_run(const Shape& s, const void* prepared, const float* in, float* out, 
              float* loss_terms = nullptr);
 int valu_loss_blocks(const Shape& s, int64_t B);  // per-block loss partials of the fused eval
 bool sgpr_enabled(const Shape& s);
-int64_t sgpr_blocks(int64_t B);
+int64_t sgpr_blocks(const Shape& s, int64_t B);
 int sgpr_run(const Shape& s, const void* prepared, const float* in, float* out, float* ld,
              float* all, int64_t B, bool inverse, hipStream_t st, const int64_t* y,
              float* loss_ws, int kind, float det, float* loss_terms);

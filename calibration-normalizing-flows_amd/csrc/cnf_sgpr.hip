@@ -11,14 +11,22 @@
 //     with no VGPR copies of weights and no LDS broadcast traffic;
 //   * the scalar-cache round trip of a Linear overlaps the previous Linear's
 //     FMAs instead of stalling the wave once per output neuron.
+// The s-net's last Linear is stored pre-multiplied by log2(e) (cnf_prepare), so
+// exp(s) is one v_exp_f32 and the log-det is ln2 * sum(s') once per row.
 // Non-strict only (strict_nan keeps k_valu); shift must be on (NICE: s = 0).
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <mutex>
+#include <unordered_map>
 
 #include "cnf_internal.h"
 #include "cnf_valu_common.h"
 #include "cnf_valu_io.h"
+
+#ifndef CNF_SGPR_WPE
+#define CNF_SGPR_WPE 5
+#endif
 
 namespace cnf {
 namespace {
@@ -32,7 +40,10 @@ struct SP {
   static constexpr int NL = H1 == 0 ? 1 : (H2 == 0 ? 2 : 3);
   static constexpr int nin(int i) { return i == 0 ? DC : (i == 1 ? H1 : H2); }
   static constexpr int nout(int i) { return i == NL - 1 ? DT : (i == 0 ? H1 : H2); }
-  static constexpr int fl(int i) { return pad16(nin(i) * nout(i) + nout(i)); }
+  // per output row: [w_o0, b_o, w_o1 .. w_o(nin-1)], row stride even so that
+  // (w_o0, b_o) is one aligned SGPR pair
+  static constexpr int stride(int i) { return (nin(i) + 2) & ~1; }
+  static constexpr int fl(int i) { return pad16(nout(i) * stride(i)); }
   static constexpr int off(int i) { return i == 0 ? 0 : off(i - 1) + fl(i - 1); }
   static constexpr int NF = off(NL);
   static constexpr int mx(int i) { return i == NL ? 0 : (fl(i) > mx(i + 1) ? fl(i) : mx(i + 1)); }
@@ -44,7 +55,19 @@ template <int NC>
 struct SW {
   v16f c[NC];
   __device__ __forceinline__ float operator[](int i) const { return c[i >> 4][i & 15]; }
+  __device__ __forceinline__ f2 pair(int i) const {  // i even
+    return f2{c[i >> 4][i & 15], c[i >> 4][(i & 15) + 1]};
+  }
 };
+
+// w0 * x + b with (w0, b) ONE SGPR pair: op_sel broadcasts the low half as the
+// multiplier and the high half as the addend, so the bias costs no VALU move
+// (a pair read twice is one constant-bus operand).
+__device__ __forceinline__ f2 fma_wb(f2 wb, f2 x) {
+  f2 a;
+  asm("v_pk_fma_f32 %0, %1, %2, %1 op_sel:[0,0,1] op_sel_hi:[0,1,1]" : "=v"(a) : "s"(wb), "v"(x));
+  return a;
+}
 
 // Issue the loads only; swait() is the point the values become usable.  The
 // wait names the buffer as an in/out operand, so no use is scheduled above it.
@@ -66,14 +89,16 @@ __device__ __forceinline__ void swait(SW<NC>& r) {
   }
 }
 
-// y[o] = b[o] + sum_k W[o][k] x[k] from an SGPR block laid out W[NOUT][NIN], b[NOUT]
-template <int NIN, int NOUT, bool RELU, int NC, class T>
+// y[o] = b[o] + sum_k W[o][k] x[k] from an SGPR block of rows
+// [w_o0, b_o, w_o1 .. w_o(NIN-1)] at stride S (even)
+template <int NIN, int NOUT, int S, bool RELU, int NC, class T>
 __device__ __forceinline__ void slin(const SW<NC>& w, const T* x, T* y) {
+  static_assert(sizeof(T) == 8, "pipelined-scalar kernel packs two rows per lane");
 #pragma unroll
   for (int o = 0; o < NOUT; ++o) {
-    T a = splat(w[NOUT * NIN + o], T{});
+    T a = fma_wb(w.pair(o * S), x[0]);
 #pragma unroll
-    for (int k = 0; k < NIN; ++k) a = fmaT(w[o * NIN + k], x[k], a);
+    for (int k = 1; k < NIN; ++k) a = fmaT(w[o * S + 1 + k], x[k], a);
     y[o] = RELU ? relu<false>(a) : a;
   }
 }
@@ -93,7 +118,7 @@ __device__ __forceinline__ void run_seq(const T* c, T* h1, T* h2, T* s, T* t, SW
     constexpr bool last = i == S::NL - 1;
     const T* in = i == 0 ? c : (i == 1 ? h1 : h2);
     T* out = last ? ((NETS == 2 && net == 0) ? s : t) : (i == 0 ? h1 : h2);
-    slin<S::nin(i), S::nout(i), !last>(cur, in, out);
+    slin<S::nin(i), S::nout(i), S::stride(i), !last>(cur, in, out);
     swait(nxt);
     cur = nxt;
     run_seq<S, NETS, IDX + 1>(c, h1, h2, s, t, cur, wl, wn);
@@ -122,11 +147,11 @@ __device__ __forceinline__ void sp_step(T* v, T& ld, SW<SP<D, H1, H2>::NC>& cur,
     T& x = v[R<D, OC>(j)];
     if constexpr (NETS == 1) {  // scale=False: s = 0, exp(0) = 1, log-det += 0
       x = INV ? x - t[j] : x + t[j];
-    } else if constexpr (!INV) {
-      x = fmaV(x, expT<true>(s[j]), t[j]);
+    } else if constexpr (!INV) {  // s[j] = log2(e) * s (scaled at prepare): exp(s) = 2^s[j]
+      x = fmaV(x, exp2T(s[j]), t[j]);
       ld += s[j];
     } else {
-      x = (x - t[j]) * expT<true>(-s[j]);
+      x = (x - t[j]) * exp2T(-s[j]);
       ld -= s[j];
     }
   }
@@ -135,13 +160,34 @@ __device__ __forceinline__ void sp_step(T* v, T& ld, SW<SP<D, H1, H2>::NC>& cur,
   }
 }
 
-template <int D, int H1, int H2, bool INV, int NETS, int RW, int ROWS>
-__global__ __launch_bounds__(ROWS, 4) void k_sgpr(
+// Async copy of one full input tile (TF floats, 16-B aligned) into LDS: every
+// wave moves 1 KiB per global_load_lds_dwordx4, lane-linear (the tile is
+// contiguous in HBM and in LDS, so the image is the row-major tile itself).
+template <int ROWS, int TF>
+__device__ __forceinline__ void tile_prefetch(float* sm, const float* __restrict__ src) {
+  static_assert(TF % 4 == 0, "tile must be whole float4s");
+  constexpr int N4 = TF / 4, NI = (N4 + 63) / 64, NW = ROWS / 64;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < (NI + NW - 1) / NW; ++i) {
+    const int c = (i * NW + w) * 64;  // first float4 of this wave's 1 KiB
+    if (c + lane < N4)
+      __builtin_amdgcn_global_load_lds(src + (int64_t)(c + lane) * 4,
+                                       (__attribute__((address_space(3))) void*)(sm + c * 4), 16,
+                                       0, 0);
+  }
+}
+
+// PIPE: persistent grid (CUs x resident blocks) walking the tiles; while a
+// tile computes, the next full tile streams into the LDS tile by LDS-DMA (no
+// VGPRs), and outputs go straight from registers to HBM.
+template <int D, int H1, int H2, bool INV, int NETS, int RW, int ROWS, bool PIPE>
+__global__ __launch_bounds__(ROWS, INV ? CNF_SGPR_WPE - 1 : CNF_SGPR_WPE) void k_sgpr(
     const float* __restrict__ W, const int32_t* __restrict__ qtab,
     const int32_t* __restrict__ lflag, const float* __restrict__ in, float* __restrict__ out,
     float* __restrict__ ld_out, float*, int64_t B, int L, int, int,
     int any_perm, int vec_io, const int64_t* __restrict__ yl, float* __restrict__ loss_part,
-    int kind, float det, unsigned*, float*) {
+    int kind, float det, unsigned* __restrict__ ticket, float* __restrict__ loss_terms) {
   using S = SP<D, H1, H2>;
   using T = typename RowT<RW>::type;
   constexpr int TR = ROWS * RW;
@@ -154,20 +200,37 @@ __global__ __launch_bounds__(ROWS, 4) void k_sgpr(
   auto layer_of = [&](int i) { return INV ? L - 1 - i : i; };
   float lt0 = 0.f, lt1 = 0.f, lt2 = 0.f;
 
+  constexpr int TF = TR * D;
+  const int64_t nfull = B / TR;
+  const bool dma = PIPE && vec;
+  if (dma && (int64_t)blockIdx.x < nfull) tile_prefetch<ROWS, TF>(sm, in + (int64_t)blockIdx.x * TF);
+
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int64_t row0 = tile * TR;
     const int nrows = (int)((B - row0) < TR ? (B - row0) : TR);
     SW<S::NC> cur;
     sissue(cur, W + (int64_t)layer_of(0) * LF);  // lands while the tile loads
-    lds_barrier();
-    tile_load<ROWS>(sm, in + row0 * D, nrows * D, vec);
     int yv[RW];
     if (loss_part) load_labels<RW>(yl, row0, tid, ROWS, B, yv);
-    lds_barrier();
-    swait(cur);
+    if (dma && tile < nfull) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA has landed
+      lds_barrier();                                    // ... and every other wave's
+    } else {
+      lds_barrier();
+      tile_load<ROWS>(sm, in + row0 * D, nrows * D, vec);
+      lds_barrier();
+    }
     T v[D];
 #pragma unroll
     for (int k = 0; k < D; ++k) v[k] = get_row<ROWS>(sm, tid, D, k, T{});
+    if (dma) {
+      const int64_t nt = tile + gridDim.x;
+      if (nt < nfull) {
+        lds_barrier();  // every wave has its rows in registers
+        tile_prefetch<ROWS, TF>(sm, in + nt * TF);
+      }
+    }
+    swait(cur);
     T ld = splat(0.f, T{});
     int i = 0;
     for (; i + 1 < L; i += 2) {
@@ -186,9 +249,16 @@ __global__ __launch_bounds__(ROWS, 4) void k_sgpr(
       sp_step<D, H1, H2, INV, false, NETS>(v, ld, cur, W + (int64_t)la * LF,
                                            W + (int64_t)layer_of(0) * LF, pa, qtab + la * D);
     }
+    if constexpr (NETS == 2) ld = ld * splat(0.69314718055994531f, T{});  // sum(s) = ln2 * sum(s')
     if (out) {
-      if (odd) store_rows<D, ROWS, true>(out + row0 * D, sm, v, nrows, vec);
-      else store_rows<D, ROWS, false>(out + row0 * D, sm, v, nrows, vec);
+      if constexpr (PIPE) {  // the LDS tile is already the next tile's DMA target
+        const bool al8 = (reinterpret_cast<uintptr_t>(out) & 7) == 0;
+        if (odd) store_rows_direct<D, ROWS, true>(out + row0 * D, v, nrows, al8);
+        else store_rows_direct<D, ROWS, false>(out + row0 * D, v, nrows, al8);
+      } else {
+        if (odd) store_rows<D, ROWS, true>(out + row0 * D, sm, v, nrows, vec);
+        else store_rows<D, ROWS, false>(out + row0 * D, sm, v, nrows, vec);
+      }
     }
     if (ld_out) store_ld<ROWS>(ld_out, row0, tid, nrows, ld);
     if (loss_part) {
@@ -196,7 +266,12 @@ __global__ __launch_bounds__(ROWS, 4) void k_sgpr(
       else tile_loss<D, false>(v, ld, yv, kind, det, lt0, lt1, lt2);
     }
   }
-  if (loss_part) block_sum3<ROWS>(lt0, lt1, lt2, smem, loss_part);
+  if (loss_part) {
+    if (ticket)  // persistent grid: one hand-off per block, no second launch
+      block_sum3_last<ROWS>(lt0, lt1, lt2, smem, loss_part, ticket, loss_terms, gridDim.x);
+    else
+      block_sum3<ROWS>(lt0, lt1, lt2, smem, loss_part);
+  }
 }
 
 using KFn = void (*)(const float*, const int32_t*, const int32_t*, const float*, float*, float*,
@@ -207,13 +282,14 @@ constexpr int kRW = 2, kRows = 256;
 
 struct SEntry {
   int D, H1, H2;
-  KFn fn[2][2];  // [nets - 1][inverse]
+  KFn fn[2][2][2];  // [pipe][nets - 1][inverse]
 };
 
-#define CNF_SGPR(D, H1, H2)                                                              \
-  {D, H1, H2,                                                                            \
-   {{k_sgpr<D, H1, H2, false, 1, kRW, kRows>, k_sgpr<D, H1, H2, true, 1, kRW, kRows>},   \
-    {k_sgpr<D, H1, H2, false, 2, kRW, kRows>, k_sgpr<D, H1, H2, true, 2, kRW, kRows>}}}
+// (the inverse never takes the LDS-DMA form, see sgpr_run)
+#define CNF_SGPR_P(D, H1, H2, P)                                                          \
+  {{k_sgpr<D, H1, H2, false, 1, kRW, kRows, P>, k_sgpr<D, H1, H2, true, 1, kRW, kRows, false>}, \
+   {k_sgpr<D, H1, H2, false, 2, kRW, kRows, P>, k_sgpr<D, H1, H2, true, 2, kRW, kRows, false>}}
+#define CNF_SGPR(D, H1, H2) {D, H1, H2, {CNF_SGPR_P(D, H1, H2, false), CNF_SGPR_P(D, H1, H2, true)}}
 
 // every shape of the VALU table whose Linears fit the 32-float buffer
 const SEntry kSTable[] = {
@@ -241,7 +317,46 @@ bool sgpr_enabled(const Shape& s) {
   return !(e && e[0] == '0');
 }
 
-int64_t sgpr_blocks(int64_t B) { return (B + kRW * kRows - 1) / (kRW * kRows); }
+static bool pipe_on() {
+  const char* e = std::getenv("CNF_SGPR_PIPE");  // A/B switch: 0 = one tile per block
+  return !(e && e[0] == '0');
+}
+
+static size_t lds_bytes(const Shape& s, bool pipe) {
+  size_t lds = (size_t)kRW * kRows * s.D * 4;
+  if (lds < (size_t)3 * kRows * 4 + 4 * 65) lds = (size_t)3 * kRows * 4 + 4 * 65;
+  return lds;
+}
+
+static int resident(KFn fn, size_t lds) {
+  static std::mutex mu;
+  static std::unordered_map<const void*, int> cache;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = cache.find((const void*)fn);
+  if (it != cache.end()) return it->second;
+  int n = 0, dev = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kRows, lds) != hipSuccess || n < 1)
+    n = 1;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      cus < 1)
+    cus = 256;
+  cache[(const void*)fn] = n * cus;
+  return n * cus;
+}
+
+static KFn pick(const SEntry* e, const Shape& s, bool inverse, bool pipe) {
+  return e->fn[pipe ? 1 : 0][s.scale ? 1 : 0][inverse ? 1 : 0];
+}
+
+int64_t sgpr_blocks(const Shape& s, int64_t B) {
+  const int64_t ntiles = (B + kRW * kRows - 1) / (kRW * kRows);
+  const SEntry* e = find(s);
+  if (!e || !pipe_on()) return ntiles;
+  // the grid does not depend on the direction: both directions share one table row
+  const int cap = resident(pick(e, s, false, true), lds_bytes(s, true));
+  return ntiles < cap ? ntiles : cap;
+}
 
 int sgpr_run(const Shape& s, const void* prepared, const float* in, float* out, float* ld,
              float* all, int64_t B, bool inverse, hipStream_t st, const int64_t* y,
@@ -256,14 +371,21 @@ int sgpr_run(const Shape& s, const void* prepared, const float* in, float* out, 
   const float* W = reinterpret_cast<const float*>(base + idx_bytes(s)) + s.sp_region;
   auto al = [](const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   const int vec = al(in) && al(out) && al(all);
-  KFn fn = e->fn[s.scale ? 1 : 0][inverse ? 1 : 0];
-  const int64_t nblk = sgpr_blocks(B);
-  size_t lds = (size_t)kRW * kRows * s.D * 4;
-  if (lds < (size_t)3 * kRows * 4 + 4 * 65) lds = (size_t)3 * kRows * 4 + 4 * 65;
+  // the inverse keeps one tile per block: its LDS-DMA form needs more VGPRs
+  // than the 5-wave bound allows (measured: scratch spills, 2x slower)
+  const bool pipe = pipe_on() && !inverse;
+  KFn fn = pick(e, s, inverse, pipe);
+  const int64_t nblk = pipe ? sgpr_blocks(s, B) : (B + kRW * kRows - 1) / (kRW * kRows);
+  const size_t lds = lds_bytes(s, pipe);
+  // one-launch loss hand-off on the persistent grid (workspace ticket word,
+  // zeroed by the caller once; the last block resets it)
+  const char* lt = std::getenv("CNF_LOSS_TICKET");
+  const bool fused = loss_ws && pipe && lt && lt[0] == '1';  // measured slower: off
   hipLaunchKernelGGL(fn, dim3((unsigned)nblk), dim3(kRows), lds, st, W, inverse ? inv_q : fwd_q,
                      flags, in, out, ld, all, B, s.L, s.scale, s.shift, s.any_perm ? 1 : 0, vec,
-                     y, loss_ws ? loss_ws + 4 : nullptr, kind, det, nullptr, nullptr);
-  if (loss_ws) reduce_partials(loss_ws + 4, (int)nblk, 4, 0, nullptr, loss_terms, st);
+                     y, loss_ws ? loss_ws + 4 : nullptr, kind, det,
+                     fused ? reinterpret_cast<unsigned*>(loss_ws) : nullptr, loss_terms);
+  if (loss_ws && !fused) reduce_partials(loss_ws + 4, (int)nblk, 4, 0, nullptr, loss_terms, st);
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) {
     set_hip_error(err);

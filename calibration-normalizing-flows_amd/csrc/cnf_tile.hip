@@ -230,6 +230,7 @@ struct PrepSeg {
   int64_t dst;  // float offset in the weights region
   int mode;     // 0: natural copy, 1: MFMA tiles, 2: compact (VALU), 3: packed (SGPR)
   int nout_full, nin_full, in_off, nin, nout, OT, KS;
+  float mul;  // mode 3: weights and bias scaled by this (log2 e on the s-net's last Linear)
 };
 
 struct PrepArgs {
@@ -256,16 +257,18 @@ __global__ void k_prepare(PrepArgs a, float* __restrict__ wreg, int32_t* __restr
       dst[i] = i < nW ? g.W[i] : g.b[i - nW];
     return;
   }
-  if (g.mode == 3) {  // W[nout][nin] (inputs from in_off) then b[nout], zero padded
-    const int64_t nW = (int64_t)g.nout * g.nin;
-    const int64_t n = (nW + g.nout + 15) & ~15;
+  if (g.mode == 3) {  // rows [w_o0, b_o, w_o1 .. w_o(nin-1)] at even stride, zero padded
+    const int S = (g.nin + 2) & ~1;
+    const int64_t n = ((int64_t)g.nout * S + 15) & ~15;
     for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
       float v = 0.f;
-      if (i < nW) {
-        const int o = (int)(i / g.nin), k = (int)(i - (int64_t)o * g.nin);
-        v = g.W[(int64_t)o * g.nin_full + g.in_off + k];
-      } else if (i - nW < g.nout) {
-        v = g.b[i - nW];
+      const int o = (int)(i / S), j = (int)(i - (int64_t)o * S);
+      if (o < g.nout) {
+        if (j == 1) v = g.b[o] * g.mul;
+        else if (j == 0 || j <= g.nin) {
+          const int k = j == 0 ? 0 : j - 1;
+          v = g.W[(int64_t)o * g.nin_full + g.in_off + k] * g.mul;
+        }
       }
       dst[i] = v;
     }
@@ -420,6 +423,8 @@ int prepare_run(const Shape& s, const float* const* params, void* prepared, hipS
         const int i = k % s.n_lin;
         g.mode = 3;
         g.nout = i == s.n_lin - 1 ? s.DT : g.nout_full;
+        // the s-net (first net when scale is on) ends in log2(e) * s
+        g.mul = (s.scale && k / s.n_lin == 0 && i == s.n_lin - 1) ? 1.4426950408889634f : 1.f;
         g.dst = d2 + (k / s.n_lin) * s.sp_net_floats + s.sp_lin_off[i];
       }
       hipLaunchKernelGGL(k_prepare, dim3(b.nseg), dim3(256), 0, st, b, wreg, idx);

@@ -314,7 +314,7 @@ static int64_t blocks_for(const Shape& s, const Variant* var, KFn fn, int64_t B)
 
 int valu_loss_blocks(const Shape& s, int64_t B) {
   if (s.valu_id < 0) return -1;
-  if (sgpr_enabled(s)) return (int)sgpr_blocks(B);
+  if (sgpr_enabled(s)) return (int)sgpr_blocks(s, B);
   const Variant* var = pick_variant(s, B);
   return (int)blocks_for(s, var, var->fn[0][s.strict ? 1 : 0], B);
 }

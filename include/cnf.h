@@ -106,9 +106,11 @@ int cnf_inverse(const cnf_desc* desc, const void* prepared, const float* z, floa
  * calibrators.py:297-317; the per-step NLL of a sharded batch):
  *   loss_terms[3]  {sum of per-row loss, sum of ce, sum of ld} over the B rows
  *   z, logdet      as cnf_forward, each may be NULL
- * Two launches on `stream`: the fused pass writes per-block partial sums into
- * the workspace, a one-block kernel adds them in block order (deterministic).
- * The workspace needs no initialisation.  Narrow flows only (valu-fused). */
+ * The fused pass writes per-block partial sums into the workspace; they are
+ * added in block order (deterministic) either by the block that finishes last
+ * (persistent grid: one launch) or by a one-block follow-up launch.  The
+ * workspace must be zero-filled before its first use; every call leaves it
+ * reusable.  Narrow flows only (valu-fused). */
 int cnf_forward_loss_workspace_bytes(const cnf_desc* desc, int64_t B, size_t* bytes);
 int cnf_forward_loss(const cnf_desc* desc, const void* prepared, const float* x,
                      const int64_t* y, int32_t loss_kind, float det, float* z, float* logdet,
@@ -145,7 +147,9 @@ int cnf_loss_vjp(const cnf_desc* desc, const void* prepared, const float* x,
                  float* loss_terms, float* grads, float* dx, int64_t B, void* workspace,
                  size_t workspace_bytes, void* stream);
 
-/* Which kernel family serves this descriptor ("valu-fused", "mfma-tile", ...). */
+/* Which kernel family serves this descriptor's final-output launches:
+ * "sgpr-fused" (pipelined scalar weights), "valu-fused" (every-layer outputs,
+ * strict_nan, and shapes whose Linears exceed 32 floats), "mfma-tile" (wide). */
 const char* cnf_kernel_name(const cnf_desc* desc);
 
 const char* cnf_strerror(int status);

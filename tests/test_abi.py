@@ -57,8 +57,10 @@ def test_cfg2_param_count_is_1740_and_cfg4_727200():
 
 def test_kernel_family_selection():
     name = lambda d: _lib.lib().cnf_kernel_name(ctypes.byref(d)).decode()
-    assert name(_lib.make_desc(10, 6, [5, 5])) == "valu-fused"
-    assert name(_lib.make_desc(3, 2, [5, 5], scale=0)) == "valu-fused"
+    assert name(_lib.make_desc(10, 6, [5, 5])) == "sgpr-fused"
+    assert name(_lib.make_desc(3, 2, [5, 5], scale=0)) == "sgpr-fused"
+    assert name(_lib.make_desc(10, 6, [5, 5], strict_nan=1)) == "valu-fused"
+    assert name(_lib.make_desc(10, 6, [10, 10])) == "valu-fused"
     assert name(_lib.make_desc(100, 12, [100, 100])) == "mfma-tile"
     assert name(_lib.make_desc(10, 3, [4, 6, 3])) == "mfma-tile"
 

@@ -54,8 +54,13 @@ def test_forward_matches_reference_fixture(name):
     assert rel_err(ld.cpu().numpy(), d["ld"]) <= TOL
     with torch.no_grad():
         z, ld2 = flow.transform(x)
-    torch.testing.assert_close(z, zs[-1], rtol=0, atol=0, equal_nan=True)
-    torch.testing.assert_close(ld2, ld, rtol=0, atol=0, equal_nan=True)
+    # final-only launches may run a different kernel (cnf_sgpr.hip: log2(e)
+    # folded into the s-net) than the every-layer launch: same result to fp32
+    # rounding, and both are held to the fixture above
+    assert rel_err(z.cpu().numpy(), d["zs"][-1]) <= TOL
+    assert rel_err(ld2.cpu().numpy(), d["ld"]) <= TOL
+    assert rel_err(z.cpu().numpy(), zs[-1].cpu().numpy()) <= TOL
+    assert rel_err(ld2.cpu().numpy(), ld.cpu().numpy()) <= TOL
 
 
 @pytest.mark.parametrize("name", [n for n in CASES if n != "g6_d4_nan"])

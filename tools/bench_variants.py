@@ -33,8 +33,10 @@ def main():
         res = {v: [] for v in VARIANTS}
         for rnd in range(5):
             for v in VARIANTS:
-                if v == 99:  # pipelined-scalar kernel (cnf_sgpr.hip)
+                if v in (97, 98, 99):  # pipelined-scalar kernel; 98/97: + LDS-DMA
                     os.environ["CNF_SGPR"] = "1"
+                    os.environ["CNF_SGPR_PIPE"] = "0" if v == 99 else "1"
+                    os.environ["CNF_LOSS_TICKET"] = "1" if v == 97 else "0"
                     os.environ.pop("CNF_VALU_VARIANT", None)
                 else:
                     os.environ["CNF_SGPR"] = "0"

@@ -21,5 +21,7 @@ run smoke 400 python -c "import __graft_entry__ as g; g.smoke()"
 run pytest_gpu 900 python -m pytest tests -m gpu -q
 TAILN=2 run bench 600 python bench.py
 run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python bench.py --steps 100 --no-cpu-baseline --no-variants
-run pmc 600 bash tools/gpu_pmc.sh $TAG cfg2 "--launches 30" "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SMEM GRBM_GUI_ACTIVE"
+rm -rf gpurun_out/pmc_${TAG}_cfg2
+run pmc 600 bash tools/gpu_pmc.sh $TAG cfg2 "--launches 30" "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SMEM GRBM_GUI_ACTIVE"
+python tools/pmc_traffic.py gpurun_out/pmc_${TAG}_cfg2 gpurun_out/${TAG}_traffic_cfg2.json cfg2 1048576 k_sgpr > /dev/null && cat gpurun_out/${TAG}_traffic_cfg2.json
 exit 0
