@@ -241,8 +241,8 @@ def cpu_baseline(w, seconds=10.0):
     return {"value": rate, "unit": "logit-vectors/sec", "cores": torch.get_num_threads(),
             "kind": "port",
             "sample": "%d x %d-vector forward passes (B=%d, D=%d, L=%d, h=%s) with the "
-                      "op-for-op torch CPU port, median; port/reference cost ratio 1.00 "
-                      "on 8 cores (DESIGN.md)" % (len(times), B, B, w["D"], w["L"], w["hidden"])}
+                      "op-for-op torch CPU port, median; port/reference time ratio 0.81-1.02 "
+                      "(profiles/r01_cpu_port_ratio.jsonl, DESIGN.md)" % (len(times), B, B, w["D"], w["L"], w["hidden"])}
 
 
 def main():

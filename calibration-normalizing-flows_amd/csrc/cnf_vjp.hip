@@ -446,45 +446,43 @@ __global__ __launch_bounds__(256) void k_reduce_cols(const float* __restrict__ p
                                   red[threadIdx.x + 128]) + red[threadIdx.x + 192];
 }
 
-// Few entries (the 3 loss sums): one 1024-thread block; thread t adds blocks
-// t, t+1024, ... in order (four independent loads in flight per entry), then
-// a fixed LDS tree -- deterministic for a given nblk.
-__global__ __launch_bounds__(1024) void k_reduce_rows(const float* __restrict__ partials,
-                                                      int nblk, int PS, int E0, int NE,
-                                                      float* __restrict__ out) {
-  constexpr int T = 1024;
-  __shared__ float red[4][T];
-  const int t = threadIdx.x;
-  float s[4] = {0.f, 0.f, 0.f, 0.f};
-  int b = t;
-  for (; b + 3 * T < nblk; b += 4 * T) {
-    float v[4][4];
+// The 3 loss sums: ONE wave.  Lane l adds blocks l, l+64, ... in order (eight
+// blocks' loads in flight per batch), then a fixed xor-butterfly over the 64
+// lanes -- no LDS, no barrier; deterministic for a given nblk.  This launch
+// sits on the critical path after the main pass, so its latency is the cost.
+__global__ __launch_bounds__(64) void k_reduce_rows(const float* __restrict__ partials, int nblk,
+                                                    int PS, int E0, int NE,
+                                                    float* __restrict__ out) {
+  const int l = threadIdx.x;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+  for (int b0 = l; b0 < nblk; b0 += 8 * 64) {
+    float v[8][3];
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        v[k][e] = e < NE ? partials[(int64_t)(b + k * T) * PS + E0 + e] : 0.f;
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) s[e] += v[k][e];
-  }
-  for (; b < nblk; b += T) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-      if (e < NE) s[e] += partials[(int64_t)b * PS + E0 + e];
-  }
-#pragma unroll
-  for (int e = 0; e < 4; ++e) red[e][t] = s[e];
-  __syncthreads();
-  for (int w = T / 2; w >= 1; w >>= 1) {
-    if (t < w) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) red[e][t] += red[e][t + w];
+    for (int k = 0; k < 8; ++k) {
+      const int b = b0 + k * 64;
+      const float* p = partials + (int64_t)b * PS + E0;
+      v[k][0] = b < nblk ? p[0] : 0.f;
+      v[k][1] = b < nblk && NE > 1 ? p[1] : 0.f;
+      v[k][2] = b < nblk && NE > 2 ? p[2] : 0.f;
     }
-    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      s0 += v[k][0];
+      s1 += v[k][1];
+      s2 += v[k][2];
+    }
   }
-  if (t < NE) out[t] = red[t][0];
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    s0 += __shfl_xor(s0, off);
+    s1 += __shfl_xor(s1, off);
+    s2 += __shfl_xor(s2, off);
+  }
+  if (l == 0) {
+    out[0] = s0;
+    if (NE > 1) out[1] = s1;
+    if (NE > 2) out[2] = s2;
+  }
 }
 
 using VFn = void (*)(const float*, const int32_t*, const int32_t*, const int32_t*, const float*,
@@ -536,7 +534,7 @@ int reduce_partials(const float* partials, int nblk, int PS, int P, float* grads
     hipLaunchKernelGGL(k_reduce_cols, dim3((unsigned)((P + 63) / 64)), dim3(256), 0, st,
                        partials, nblk, PS, P, grads);
   if (terms)
-    hipLaunchKernelGGL(k_reduce_rows, dim3(1), dim3(1024), 0, st, partials, nblk, PS, P, 3,
+    hipLaunchKernelGGL(k_reduce_rows, dim3(1), dim3(64), 0, st, partials, nblk, PS, P, 3,
                        terms);
   return CNF_OK;
 }

@@ -141,6 +141,7 @@ def _logits(B, D, seed):
 
 @pytest.mark.parametrize("D,L,hidden,B,sigma,flip", [
     (10, 6, [5, 5], 1 << 20, 0.1, False),        # cfg2 / cfg5 at full size
+    (10, 6, [5, 5], 1 << 23, 0.1, False),        # 8M rows: many tiles per persistent block
     (10, 6, [5, 5], 1000003, 0.2, True),         # ragged batch, random_flip
     (3, 2, [5, 5], 1 << 20, 0.2, False),         # cfg1 shape, RealNVP
     (100, 12, [100, 100], 1 << 16, 0.03, False), # cfg4
@@ -194,7 +195,7 @@ def test_nonaligned_input_view():
 def test_fused_forward_loss_matches_oracle(kind):
     flow = _make_flow(10, 6, [5, 5], 0.1, 9)
     stack = flow._native_stack()
-    for B in (1, 1000, 1 << 20):
+    for B in (1, 1000, 1 << 20, (1 << 23) + 77):
         x = _logits(B, 10, 11)
         y = torch.randint(0, 10, (B,), device=DEV, generator=torch.Generator(device=DEV).manual_seed(5))
         terms, z, ld = stack.forward_loss(x, y, kind=kind, det=0.5, want_outputs=True)
