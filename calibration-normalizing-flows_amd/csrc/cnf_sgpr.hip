@@ -354,8 +354,19 @@ int64_t sgpr_blocks(const Shape& s, int64_t B) {
   const SEntry* e = find(s);
   if (!e || !pipe_on()) return ntiles;
   // the grid does not depend on the direction: both directions share one table row
-  const int cap = resident(pick(e, s, false, true), lds_bytes(s, true));
-  return ntiles < cap ? ntiles : cap;
+  int cap = resident(pick(e, s, false, true), lds_bytes(s, true));
+  if (const char* g = std::getenv("CNF_SGPR_GRID")) {  // experiment: fixed grid cap
+    const int n = std::atoi(g);
+    if (n > 0) cap = n;
+  }
+  if (ntiles <= cap) return ntiles;
+  // balanced: the smallest grid that still gives every block the same tile
+  // count (1M rows: 2,048 tiles on 1,024 blocks x 2, not 1,280 blocks x 1-2)
+  // (measured slower: 4 waves/SIMD hide less than 5, so it stays opt-in)
+  const char* b = std::getenv("CNF_SGPR_BAL");  // A/B switch: 1 = balanced grid
+  if (!(b && b[0] == '1')) return cap;
+  const int64_t per = (ntiles + cap - 1) / cap;
+  return (ntiles + per - 1) / per;
 }
 
 int sgpr_run(const Shape& s, const void* prepared, const float* in, float* out, float* ld,

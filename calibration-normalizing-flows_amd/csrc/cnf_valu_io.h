@@ -135,6 +135,27 @@ __device__ __forceinline__ void load_labels(const int64_t* __restrict__ yl, int6
   }
 }
 
+// z[y] by a binary select tree on the label's bits, all integer bit work:
+// per level one v_bfe_i32 turns bit b of y into a 0 / -1 mask and each pair is
+// merged by one v_bfi_b32 -- ceil(log2 D) + D - 1 VALU per row, no lane masks
+// (so no VCC hazard nops), no branches, and no select chain for LLVM to fold
+// into a scratch-indexed load.  Labels outside [0, D) pick 0, as a linear
+// scan would.
+template <int N>
+__device__ __forceinline__ uint32_t sel_tree(const uint32_t* a, int y, int bit) {
+  if constexpr (N == 1) {
+    return a[0];
+  } else {
+    constexpr int M = (N + 1) / 2;
+    uint32_t b[M];
+    const uint32_t m = (uint32_t)((y << (31 - bit)) >> 31);  // arithmetic: 0 or ~0
+#pragma unroll
+    for (int p = 0; p < N / 2; ++p) b[p] = (m & a[2 * p + 1]) | (~m & a[2 * p]);
+    if constexpr (N & 1) b[M - 1] = a[N - 1];
+    return sel_tree<M>(b, y, bit + 1);
+  }
+}
+
 template <int D, bool O, class T>
 __device__ __forceinline__ void tile_loss(const T* v, T ld, const int* y, int kind, float det,
                                           float& t0, float& t1, float& t2) {
@@ -146,11 +167,14 @@ __device__ __forceinline__ void tile_loss(const T* v, T ld, const int* y, int ki
   const T nm = m * splat(-kL2E, T{});
   T se = splat(0.f, T{}), zy = splat(0.f, T{});
 #pragma unroll
-  for (int j = 0; j < D; ++j) {
-    const T zj = v[R<D, O>(j)];
-    se += exp2T(fmaT(kL2E, zj, nm));
+  for (int j = 0; j < D; ++j) se += exp2T(fmaT(kL2E, v[R<D, O>(j)], nm));
 #pragma unroll
-    for (int q = 0; q < RW; ++q) setc(zy, q, comp(zy, q) + (j == y[q] ? comp(zj, q) : 0.f));
+  for (int q = 0; q < RW; ++q) {
+    uint32_t zq[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) zq[j] = __float_as_uint(comp(v[R<D, O>(j)], q));
+    const float pk = __uint_as_float(sel_tree<D>(zq, y[q], 0));
+    setc(zy, q, (unsigned)y[q] < (unsigned)D ? pk : 0.f);
   }
 #pragma unroll
   for (int q = 0; q < RW; ++q) {

@@ -24,6 +24,8 @@
 // block order -- no float atomics, bit-reproducible run to run.
 #include <hip/hip_runtime.h>
 
+#include <cstdint>
+#include <cstdlib>
 #include <type_traits>
 
 #include "cnf_internal.h"
@@ -485,6 +487,51 @@ __global__ __launch_bounds__(64) void k_reduce_rows(const float* __restrict__ pa
   }
 }
 
+// Loss-term sums of 16-B partial records ([t0, t1, t2, pad] per block, the
+// forward-loss kernels' layout): four waves, one float4 per record, up to
+// eight records per lane in flight before the first add, so a 2,048-block grid
+// is one round of load latency instead of four.  Fixed order throughout
+// (lane-strided sums, xor butterfly, waves in index order): deterministic.
+constexpr int kRR = 256;
+__global__ __launch_bounds__(kRR) void k_reduce_rows4(const float4* __restrict__ partials,
+                                                      int nblk, float* __restrict__ out) {
+  __shared__ float red[kRR / 64][3];
+  const int t = threadIdx.x;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+  for (int b0 = t; b0 < nblk; b0 += 8 * kRR) {
+    float4 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int b = b0 + k * kRR;
+      v[k] = b < nblk ? partials[b] : float4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      s0 += v[k].x;
+      s1 += v[k].y;
+      s2 += v[k].z;
+    }
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    s0 += __shfl_xor(s0, off);
+    s1 += __shfl_xor(s1, off);
+    s2 += __shfl_xor(s2, off);
+  }
+  if ((t & 63) == 0) {
+    red[t >> 6][0] = s0;
+    red[t >> 6][1] = s1;
+    red[t >> 6][2] = s2;
+  }
+  __syncthreads();
+  if (t < 3) {
+    float a = 0.f;
+#pragma unroll
+    for (int w = 0; w < kRR / 64; ++w) a += red[w][t];
+    out[t] = a;
+  }
+}
+
 using VFn = void (*)(const float*, const int32_t*, const int32_t*, const int32_t*, const float*,
                      const int64_t*, const float*, const float*, const float*, float*, float*,
                      int64_t, int, int, int, int, int, float, float, int, int);
@@ -533,7 +580,13 @@ int reduce_partials(const float* partials, int nblk, int PS, int P, float* grads
   if (P > 0)
     hipLaunchKernelGGL(k_reduce_cols, dim3((unsigned)((P + 63) / 64)), dim3(256), 0, st,
                        partials, nblk, PS, P, grads);
-  if (terms)
+  const char* e = std::getenv("CNF_REDUCE4");  // A/B switch: 0 = one-wave k_reduce_rows
+  const bool r4 = PS == 4 && P == 0 && (reinterpret_cast<uintptr_t>(partials) & 15) == 0 &&
+                  !(e && e[0] == '0');
+  if (terms && r4)
+    hipLaunchKernelGGL(k_reduce_rows4, dim3(1), dim3(kRR), 0, st,
+                       reinterpret_cast<const float4*>(partials), nblk, terms);
+  else if (terms)
     hipLaunchKernelGGL(k_reduce_rows, dim3(1), dim3(64), 0, st, partials, nblk, PS, P, 3,
                        terms);
   return CNF_OK;
