@@ -28,10 +28,32 @@
 #define CNF_SGPR_WPE 5
 #endif
 
+#ifdef CNF_TIMELINE
+// Diagnostic build only (make timeline): per-block wall-clock marks of the
+// persistent kernel, s_memrealtime (100 MHz): [start, first tile ready, end, hw id]
+__device__ unsigned long long cnf_tl[4096 * 4];
+#endif
+
 namespace cnf {
 namespace {
 
 using namespace valu;
+
+#ifdef CNF_TIMELINE
+__device__ __forceinline__ void tl_mark(int slot) {
+  if (threadIdx.x == 0 && blockIdx.x < 4096) {
+    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+    cnf_tl[blockIdx.x * 4 + slot] = t;
+    if (slot == 0)
+      cnf_tl[blockIdx.x * 4 + 3] =
+          ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
+          __builtin_amdgcn_s_getreg((31 << 11) | 4);  // XCC_ID, HW_ID
+  }
+}
+#define CNF_TL(slot) tl_mark(slot)
+#else
+#define CNF_TL(slot)
+#endif
 
 // Compile-time SP layout of one net (must match derive_shape's sp_lin_off).
 template <int D, int H1, int H2>
@@ -69,30 +91,38 @@ __device__ __forceinline__ f2 fma_wb(f2 wb, f2 x) {
   return a;
 }
 
-// Issue the loads only; swait() is the point the values become usable.  The
-// wait names the buffer as an in/out operand, so no use is scheduled above it.
+// Issue the loads of one Linear block: plain (compiler-visible) scalar loads,
+// so the compiler's own s_waitcnt insertion guards every read of the
+// destination SGPRs -- including any copy or spill the register allocator
+// adds -- and a sched_barrier keeps the load from sinking toward its use:
+// ALU work may cross it, memory operations may not, so the block's
+// s_load_dwordx16 pair issues one Linear ahead of its first FMA.
+// (An earlier form issued the s_load from inline asm and waited in a second
+// asm statement; the allocator was then free to copy the in-flight
+// destination registers between the two -- seen as s_mov_b64 of a pending
+// s_load_dwordx16 destination -- i.e. to read weights before they landed.)
 template <int NC>
 __device__ __forceinline__ void sissue(SW<NC>& r, const float* p) {
-  if constexpr (NC == 1) {
-    asm volatile("s_load_dwordx16 %0, %1, 0x0" : "=s"(r.c[0]) : "s"(p));
-  } else {
-    asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx16 %1, %2, 0x40"
-                 : "=&s"(r.c[0]), "=s"(r.c[1]) : "s"(p));
-  }
+  const v16f* q = reinterpret_cast<const v16f*>(__builtin_assume_aligned(p, 64));
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int i = 0; i < NC; ++i) r.c[i] = q[i];
+  __builtin_amdgcn_sched_barrier(0);
 }
+// End of the Linear that overlaps the load: nothing crosses, so the next
+// Linear's FMAs (the loaded block's consumers) cannot be hoisted up to the load.
 template <int NC>
-__device__ __forceinline__ void swait(SW<NC>& r) {
-  if constexpr (NC == 1) {
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(r.c[0]));
-  } else {
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(r.c[0]), "+s"(r.c[1]));
-  }
+__device__ __forceinline__ void swait(SW<NC>&) {
+  __builtin_amdgcn_sched_barrier(0);
 }
 
 // y[o] = b[o] + sum_k W[o][k] x[k] from an SGPR block of rows
 // [w_o0, b_o, w_o1 .. w_o(NIN-1)] at stride S (even)
-template <int NIN, int NOUT, int S, bool RELU, int NC, class T>
-__device__ __forceinline__ void slin(const SW<NC>& w, const T* x, T* y) {
+// after(): issued once the first output neuron is done (the next block's load:
+// the compiler's wait for THIS block then precedes it, so an SMEM lgkmcnt(0)
+// never has to cover the load just issued).
+template <int NIN, int NOUT, int S, bool RELU, int NC, class T, class F>
+__device__ __forceinline__ void slin(const SW<NC>& w, const T* x, T* y, F&& after) {
   static_assert(sizeof(T) == 8, "pipelined-scalar kernel packs two rows per lane");
 #pragma unroll
   for (int o = 0; o < NOUT; ++o) {
@@ -100,36 +130,47 @@ __device__ __forceinline__ void slin(const SW<NC>& w, const T* x, T* y) {
 #pragma unroll
     for (int k = 1; k < NIN; ++k) a = fmaT(w[o * S + 1 + k], x[k], a);
     y[o] = RELU ? relu<false>(a) : a;
+    if (o == 0) after();
   }
 }
 
 // Linear IDX of the layer's sequence (net-major: s-net Linears, then t-net);
 // the next block (or the next layer's first, wn) is issued before computing.
-template <class S, int NETS, int IDX, class T>
-__device__ __forceinline__ void run_seq(const T* c, T* h1, T* h2, T* s, T* t, SW<S::NC>& cur,
-                                        const float* wl, const float* wn) {
+// The two SGPR buffers alternate by the Linear's parity in the layer pair
+// (PAR: parity of the layer's first Linear) -- never a `cur = nxt` copy: a
+// copy gives the compiler a reason to move the in-flight destination of an
+// s_load into other registers before the s_waitcnt (seen: s_mov_b64 of a
+// pending s_load_dwordx16 destination), i.e. to read it before it lands.
+template <class S, int NETS, int IDX, int PAR, class T>
+__device__ __forceinline__ void run_seq(const T* c, T* h1, T* h2, T* s, T* t, SW<S::NC>& A,
+                                        SW<S::NC>& Bf, const float* wl, const float* wn) {
   if constexpr (IDX < NETS * S::NL) {
     constexpr int net = IDX / S::NL, i = IDX % S::NL;
-    SW<S::NC> nxt;
-    if constexpr (IDX + 1 < NETS * S::NL)
-      sissue(nxt, wl + ((IDX + 1) / S::NL) * S::NF + S::off((IDX + 1) % S::NL));
-    else
-      sissue(nxt, wn);
+    constexpr bool odd = ((IDX + PAR) & 1) != 0;
+    SW<S::NC>& cur = odd ? Bf : A;
+    SW<S::NC>& nxt = odd ? A : Bf;
     constexpr bool last = i == S::NL - 1;
     const T* in = i == 0 ? c : (i == 1 ? h1 : h2);
     T* out = last ? ((NETS == 2 && net == 0) ? s : t) : (i == 0 ? h1 : h2);
-    slin<S::nin(i), S::nout(i), S::stride(i), !last>(cur, in, out);
+    slin<S::nin(i), S::nout(i), S::stride(i), !last>(cur, in, out, [&]() {
+      if constexpr (IDX + 1 < NETS * S::NL)
+        sissue(nxt, wl + ((IDX + 1) / S::NL) * S::NF + S::off((IDX + 1) % S::NL));
+      else
+        sissue(nxt, wn);
+    });
     swait(nxt);
-    cur = nxt;
-    run_seq<S, NETS, IDX + 1>(c, h1, h2, s, t, cur, wl, wn);
+    run_seq<S, NETS, IDX + 1, PAR>(c, h1, h2, s, t, A, Bf, wl, wn);
   }
 }
 
 // One coupling layer, input in orientation O, output in orientation !O
 // (k_valu's step(), non-strict, weights from the pipelined SGPR buffer).
+// O is also the layer's position in its pair (the odd tail layer is a first):
+// the second layer's Linears start on buffer parity NETS * NL.
 template <int D, int H1, int H2, bool INV, bool O, int NETS, class T>
-__device__ __forceinline__ void sp_step(T* v, T& ld, SW<SP<D, H1, H2>::NC>& cur,
-                                        const float* wl, const float* wn, bool perm,
+__device__ __forceinline__ void sp_step(T* v, T& ld, SW<SP<D, H1, H2>::NC>& A,
+                                        SW<SP<D, H1, H2>::NC>& Bf, const float* wl,
+                                        const float* wn, bool perm,
                                         const int32_t* __restrict__ q) {
   using S = SP<D, H1, H2>;
   constexpr int DT = S::DT, DC = S::DC;
@@ -141,7 +182,7 @@ __device__ __forceinline__ void sp_step(T* v, T& ld, SW<SP<D, H1, H2>::NC>& cur,
 #pragma unroll
   for (int k = 0; k < DC; ++k) c[k] = v[R<D, OC>(DT + k)];
   T h1[H1 > 0 ? H1 : 1], h2[H2 > 0 ? H2 : 1], s[DT], t[DT];
-  run_seq<S, NETS, 0>(c, h1, h2, s, t, cur, wl, wn);
+  run_seq<S, NETS, 0, O ? (NETS * S::NL) & 1 : 0>(c, h1, h2, s, t, A, Bf, wl, wn);
 #pragma unroll
   for (int j = 0; j < DT; ++j) {
     T& x = v[R<D, OC>(j)];
@@ -178,10 +219,36 @@ __device__ __forceinline__ void tile_prefetch(float* sm, const float* __restrict
   }
 }
 
+// Per-wave form: wave w copies only the rows it owns (rows q*ROWS + 64w ..
+// +63 of the tile, RW contiguous 64*D-float chunks) into the same place of the
+// LDS image, so it waits on its own vmcnt and needs no block barrier before
+// reading them or before refilling them with the next tile.
+template <int D, int ROWS, int RW>
+__device__ __forceinline__ void wave_prefetch(float* sm, const float* __restrict__ src) {
+  constexpr int N4 = 16 * D;  // float4s per 64-row chunk
+  const int lane = threadIdx.x & 63;
+  // wave-uniform chunk bases in SGPRs; one lane-offset VGPR for every copy
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#pragma unroll
+  for (int q = 0; q < RW; ++q) {
+    const int c0 = (q * ROWS + 64 * w) * D / 4;  // first float4 of the chunk
+    const float* base = src + (int64_t)c0 * 4;
+#pragma unroll
+    for (int i = 0; i < (N4 + 63) / 64; ++i) {
+      if (i * 64 + lane < N4)
+        __builtin_amdgcn_global_load_lds(base + (i * 64 + lane) * 4,
+                                         (__attribute__((address_space(3))) void*)(sm + (c0 + i * 64) * 4),
+                                         16, 0, 0);
+    }
+  }
+}
+
 // PIPE: persistent grid (CUs x resident blocks) walking the tiles; while a
 // tile computes, the next full tile streams into the LDS tile by LDS-DMA (no
 // VGPRs), and outputs go straight from registers to HBM.
-template <int D, int H1, int H2, bool INV, int NETS, int RW, int ROWS, bool PIPE>
+// PIPE: 0 one tile per block, 1 persistent + block-wide DMA, 2 persistent +
+// per-wave DMA (no barriers on the tile path).
+template <int D, int H1, int H2, bool INV, int NETS, int RW, int ROWS, int PIPE>
 __global__ __launch_bounds__(ROWS, INV ? CNF_SGPR_WPE - 1 : CNF_SGPR_WPE) void k_sgpr(
     const float* __restrict__ W, const int32_t* __restrict__ qtab,
     const int32_t* __restrict__ lflag, const float* __restrict__ in, float* __restrict__ out,
@@ -196,6 +263,7 @@ __global__ __launch_bounds__(ROWS, INV ? CNF_SGPR_WPE - 1 : CNF_SGPR_WPE) void k
   float* sm = smem;
   const int tid = threadIdx.x;
   const bool vec = vec_io != 0;
+  CNF_TL(0);
   const int64_t ntiles = (B + TR - 1) / TR;
   auto layer_of = [&](int i) { return INV ? L - 1 - i : i; };
   float lt0 = 0.f, lt1 = 0.f, lt2 = 0.f;
@@ -203,18 +271,22 @@ __global__ __launch_bounds__(ROWS, INV ? CNF_SGPR_WPE - 1 : CNF_SGPR_WPE) void k
   constexpr int TF = TR * D;
   const int64_t nfull = B / TR;
   const bool dma = PIPE && vec;
-  if (dma && (int64_t)blockIdx.x < nfull) tile_prefetch<ROWS, TF>(sm, in + (int64_t)blockIdx.x * TF);
+  constexpr bool WDMA = PIPE == 2;
+  if (dma && (int64_t)blockIdx.x < nfull) {
+    if constexpr (WDMA) wave_prefetch<D, ROWS, RW>(sm, in + (int64_t)blockIdx.x * TF);
+    else tile_prefetch<ROWS, TF>(sm, in + (int64_t)blockIdx.x * TF);
+  }
 
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int64_t row0 = tile * TR;
     const int nrows = (int)((B - row0) < TR ? (B - row0) : TR);
-    SW<S::NC> cur;
+    SW<S::NC> cur, alt;
     sissue(cur, W + (int64_t)layer_of(0) * LF);  // lands while the tile loads
     int yv[RW];
     if (loss_part) load_labels<RW>(yl, row0, tid, ROWS, B, yv);
     if (dma && tile < nfull) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA has landed
-      lds_barrier();                                    // ... and every other wave's
+      if constexpr (!WDMA) lds_barrier();               // ... and every other wave's
     } else {
       lds_barrier();
       tile_load<ROWS>(sm, in + row0 * D, nrows * D, vec);
@@ -223,11 +295,18 @@ __global__ __launch_bounds__(ROWS, INV ? CNF_SGPR_WPE - 1 : CNF_SGPR_WPE) void k
     T v[D];
 #pragma unroll
     for (int k = 0; k < D; ++k) v[k] = get_row<ROWS>(sm, tid, D, k, T{});
+    if (tile == blockIdx.x) CNF_TL(1);
     if (dma) {
       const int64_t nt = tile + gridDim.x;
       if (nt < nfull) {
-        lds_barrier();  // every wave has its rows in registers
-        tile_prefetch<ROWS, TF>(sm, in + nt * TF);
+        if constexpr (WDMA) {
+          // this wave's rows are in registers once its LDS reads return
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          wave_prefetch<D, ROWS, RW>(sm, in + nt * TF);
+        } else {
+          lds_barrier();  // every wave has its rows in registers
+          tile_prefetch<ROWS, TF>(sm, in + nt * TF);
+        }
       }
     }
     swait(cur);
@@ -237,16 +316,16 @@ __global__ __launch_bounds__(ROWS, INV ? CNF_SGPR_WPE - 1 : CNF_SGPR_WPE) void k
       const int la = layer_of(i), lb = layer_of(i + 1), lc = layer_of(i + 2 < L ? i + 2 : 0);
       const bool pa = any_perm && (lflag[la] & kFlagPerm);
       const bool pb = any_perm && (lflag[lb] & kFlagPerm);
-      sp_step<D, H1, H2, INV, false, NETS>(v, ld, cur, W + (int64_t)la * LF,
+      sp_step<D, H1, H2, INV, false, NETS>(v, ld, cur, alt, W + (int64_t)la * LF,
                                            W + (int64_t)lb * LF, pa, qtab + la * D);
-      sp_step<D, H1, H2, INV, true, NETS>(v, ld, cur, W + (int64_t)lb * LF,
+      sp_step<D, H1, H2, INV, true, NETS>(v, ld, cur, alt, W + (int64_t)lb * LF,
                                           W + (int64_t)lc * LF, pb, qtab + lb * D);
     }
     const bool odd = i < L;
     if (odd) {
       const int la = layer_of(i);
       const bool pa = any_perm && (lflag[la] & kFlagPerm);
-      sp_step<D, H1, H2, INV, false, NETS>(v, ld, cur, W + (int64_t)la * LF,
+      sp_step<D, H1, H2, INV, false, NETS>(v, ld, cur, alt, W + (int64_t)la * LF,
                                            W + (int64_t)layer_of(0) * LF, pa, qtab + la * D);
     }
     if constexpr (NETS == 2) ld = ld * splat(0.69314718055994531f, T{});  // sum(s) = ln2 * sum(s')
@@ -266,6 +345,7 @@ __global__ __launch_bounds__(ROWS, INV ? CNF_SGPR_WPE - 1 : CNF_SGPR_WPE) void k
       else tile_loss<D, false>(v, ld, yv, kind, det, lt0, lt1, lt2);
     }
   }
+  CNF_TL(2);
   if (loss_part) {
     if (ticket)  // persistent grid: one hand-off per block, no second launch
       block_sum3_last<ROWS>(lt0, lt1, lt2, smem, loss_part, ticket, loss_terms, gridDim.x);
@@ -282,14 +362,15 @@ constexpr int kRW = 2, kRows = 256;
 
 struct SEntry {
   int D, H1, H2;
-  KFn fn[2][2][2];  // [pipe][nets - 1][inverse]
+  KFn fn[3][2][2];  // [pipe][nets - 1][inverse]
 };
 
 // (the inverse never takes the LDS-DMA form, see sgpr_run)
-#define CNF_SGPR_P(D, H1, H2, P)                                                          \
-  {{k_sgpr<D, H1, H2, false, 1, kRW, kRows, P>, k_sgpr<D, H1, H2, true, 1, kRW, kRows, false>}, \
-   {k_sgpr<D, H1, H2, false, 2, kRW, kRows, P>, k_sgpr<D, H1, H2, true, 2, kRW, kRows, false>}}
-#define CNF_SGPR(D, H1, H2) {D, H1, H2, {CNF_SGPR_P(D, H1, H2, false), CNF_SGPR_P(D, H1, H2, true)}}
+#define CNF_SGPR_P(D, H1, H2, P)                                                      \
+  {{k_sgpr<D, H1, H2, false, 1, kRW, kRows, P>, k_sgpr<D, H1, H2, true, 1, kRW, kRows, 0>}, \
+   {k_sgpr<D, H1, H2, false, 2, kRW, kRows, P>, k_sgpr<D, H1, H2, true, 2, kRW, kRows, 0>}}
+#define CNF_SGPR(D, H1, H2) \
+  {D, H1, H2, {CNF_SGPR_P(D, H1, H2, 0), CNF_SGPR_P(D, H1, H2, 1), CNF_SGPR_P(D, H1, H2, 2)}}
 
 // every shape of the VALU table whose Linears fit the 32-float buffer
 const SEntry kSTable[] = {
@@ -317,10 +398,16 @@ bool sgpr_enabled(const Shape& s) {
   return !(e && e[0] == '0');
 }
 
-static bool pipe_on() {
-  const char* e = std::getenv("CNF_SGPR_PIPE");  // A/B switch: 0 = one tile per block
-  return !(e && e[0] == '0');
+// A/B switch CNF_SGPR_PIPE: 0 one tile per block, 1 block-wide DMA, 2 per-wave
+// DMA (default).  A wave-granular dynamic schedule (atomic unit counters per
+// XCD, per-unit loss records) was measured and dropped: 24% slower at 1M rows,
+// no faster at 8M.
+static int pipe_mode() {
+  const char* e = std::getenv("CNF_SGPR_PIPE");
+  if (e && e[0] >= '0' && e[0] <= '2') return e[0] - '0';
+  return 2;
 }
+static bool pipe_on() { return pipe_mode() != 0; }
 
 static size_t lds_bytes(const Shape& s, bool pipe) {
   size_t lds = (size_t)kRW * kRows * s.D * 4;
@@ -346,7 +433,7 @@ static int resident(KFn fn, size_t lds) {
 }
 
 static KFn pick(const SEntry* e, const Shape& s, bool inverse, bool pipe) {
-  return e->fn[pipe ? 1 : 0][s.scale ? 1 : 0][inverse ? 1 : 0];
+  return e->fn[pipe ? pipe_mode() : 0][s.scale ? 1 : 0][inverse ? 1 : 0];
 }
 
 int64_t sgpr_blocks(const Shape& s, int64_t B) {
@@ -406,3 +493,13 @@ int sgpr_run(const Shape& s, const void* prepared, const float* in, float* out, 
 }
 
 }  // namespace cnf
+
+#ifdef CNF_TIMELINE
+extern "C" int cnf_diag_timeline(unsigned long long* host, int n) {
+  if (n > 4096 * 4) n = 4096 * 4;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(cnf_tl), n * 8, 0, hipMemcpyDeviceToHost) ==
+                 hipSuccess
+             ? n
+             : -1;
+}
+#endif

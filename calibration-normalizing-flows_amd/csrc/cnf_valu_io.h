@@ -119,8 +119,7 @@ __device__ __forceinline__ void store_rows_direct(float* __restrict__ dst, const
 // CAL: loss = -(log(softmax(z)[y] + 1e-7) + ld)       calibrators.py:288-291
 // CE:  loss = -log_softmax(z)[y] - det * ld            run_experiment3D.py:107
 // The max / shifted-exp / sum run on whole RW-row vectors (packed FMAs);
-// z[y] is a sum of per-lane selects (a select chain over an array would be
-// folded into a dynamically indexed scratch load).
+// z[y] is picked per row by sel_tree (below).
 // Labels of the lane's RW rows (low 32-bit word of the int64 targets; -1 past
 // the batch end), issued with the tile load so the latency hides under the
 // layer sweep instead of stalling the loss at the end.
