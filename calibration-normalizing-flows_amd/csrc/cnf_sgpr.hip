@@ -252,7 +252,7 @@ template <int D, int H1, int H2, bool INV, int NETS, int RW, int ROWS, int PIPE>
 __global__ __launch_bounds__(ROWS, INV ? CNF_SGPR_WPE - 1 : CNF_SGPR_WPE) void k_sgpr(
     const float* __restrict__ W, const int32_t* __restrict__ qtab,
     const int32_t* __restrict__ lflag, const float* __restrict__ in, float* __restrict__ out,
-    float* __restrict__ ld_out, float*, int64_t B, int L, int, int,
+    float* __restrict__ ld_out, float*, int64_t B, int L, int prio_mode, int,
     int any_perm, int vec_io, const int64_t* __restrict__ yl, float* __restrict__ loss_part,
     int kind, float det, unsigned* __restrict__ ticket, float* __restrict__ loss_terms) {
   using S = SP<D, H1, H2>;
@@ -278,6 +278,13 @@ __global__ __launch_bounds__(ROWS, INV ? CNF_SGPR_WPE - 1 : CNF_SGPR_WPE) void k
   }
 
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    if (prio_mode) {  // longest-remaining-first: blocks with more tiles left win issue
+      const int64_t rem = (ntiles - 1 - tile) / gridDim.x;  // tiles after this one
+      if (rem >= 3) __builtin_amdgcn_s_setprio(3);
+      else if (rem == 2) __builtin_amdgcn_s_setprio(2);
+      else if (rem == 1) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+    }
     const int64_t row0 = tile * TR;
     const int nrows = (int)((B - row0) < TR ? (B - row0) : TR);
     SW<S::NC> cur, alt;
@@ -408,6 +415,15 @@ static int pipe_mode() {
   return 2;
 }
 static bool pipe_on() { return pipe_mode() != 0; }
+// A/B switch CNF_SGPR_PRIO (default on): s_setprio by tiles remaining on the
+// persistent grid.  The SIMD's oldest-first arbitration otherwise finishes
+// blocks far apart (tools/timeline.py: 97..231 us at 8M rows) and idles
+// through the tail; measured -4 % at 8M rows, neutral at 1M.  (Non-temporal
+// output stores were measured too: +27 % at 1M, dropped.)
+static bool prio_on() {
+  const char* e = std::getenv("CNF_SGPR_PRIO");
+  return !(e && e[0] == '0');
+}
 
 static size_t lds_bytes(const Shape& s, bool pipe) {
   size_t lds = (size_t)kRW * kRows * s.D * 4;
@@ -480,7 +496,8 @@ int sgpr_run(const Shape& s, const void* prepared, const float* in, float* out, 
   const char* lt = std::getenv("CNF_LOSS_TICKET");
   const bool fused = loss_ws && pipe && lt && lt[0] == '1';  // measured slower: off
   hipLaunchKernelGGL(fn, dim3((unsigned)nblk), dim3(kRows), lds, st, W, inverse ? inv_q : fwd_q,
-                     flags, in, out, ld, all, B, s.L, s.scale, s.shift, s.any_perm ? 1 : 0, vec,
+                     flags, in, out, ld, all, B, s.L, prio_on() ? 1 : 0, 0,
+                     s.any_perm ? 1 : 0, vec,
                      y, loss_ws ? loss_ws + 4 : nullptr, kind, det,
                      fused ? reinterpret_cast<unsigned*>(loss_ws) : nullptr, loss_terms);
   if (loss_ws && !fused) reduce_partials(loss_ws + 4, (int)nblk, 4, 0, nullptr, loss_terms, st);
