@@ -132,7 +132,7 @@ int cnf_prepared_bytes(const cnf_desc* desc, size_t* bytes) {
   if (st != CNF_OK) return st;
   if (!bytes) return CNF_ERR_NULL;
   const int64_t wf = s.family == Family::kTile
-                       ? s.tile_layer_floats * s.L
+                       ? s.tile_layer_floats * s.L + s.wide_floats
                        : s.valu_net_floats * s.nets * s.L +
                              (s.sp_ok ? s.sp_net_floats * s.nets * s.L : 0);
   // +256: scalar-cache prefetch reads whole 64-B lines past the last weight
@@ -260,7 +260,8 @@ int cnf_loss_vjp(const cnf_desc* desc, const void* prepared, const float* x, con
 const char* cnf_kernel_name(const cnf_desc* desc) {
   Shape s;
   if (derive_shape(desc, &s) != CNF_OK) return "unsupported";
-  if (s.family != Family::kValu) return "mfma-tile";
+  if (s.family != Family::kValu)
+    return s.wide_floats > 0 && wide_ok(s) ? "mfma-wide" : "mfma-tile";
   return sgpr_enabled(s) ? "sgpr-fused" : "valu-fused";
 }
 

@@ -51,6 +51,9 @@ struct Shape {
   int tile_nop = 0;                  // padded S/T rows
   int tile_waves = 0;                // waves per block that fit LDS
   size_t tile_lds_bytes = 0;
+  // register-resident MFMA layout (cnf_wide.hip), appended after the tile region
+  int64_t wide_region = 0;           // float offset of the region in the weights region
+  int64_t wide_floats = 0;           // floats of the region (0: shape not in its table)
 };
 
 // Prepared blob: [int32 fwd_q L*D][int32 inv_q L*D][int32 flags L] padded to
@@ -84,6 +87,12 @@ int tile_run(const Shape& s, const void* prepared, const float* in, float* out, 
              float* all, int64_t B, bool inverse, hipStream_t st);
 
 int prepare_run(const Shape& s, const float* const* params, void* prepared, hipStream_t st);
+
+int64_t wide_layer_floats(const Shape& s);  // 0 when the shape has no k_wide instance
+bool wide_ok(const Shape& s);               // k_wide serves this descriptor's final outputs
+int wide_prepare(const Shape& s, const float* const* params, void* prepared, hipStream_t st);
+int wide_run(const Shape& s, const void* prepared, const float* in, float* out, float* ld,
+             int64_t B, bool inverse, hipStream_t st);
 
 int vjp_workspace(const Shape& s, int64_t B, size_t* bytes);
 // kind < 0: generic VJP from gz / gz_all / gld;  kind = CNF_LOSS_*: fused loss

@@ -333,12 +333,16 @@ int tile_configure(Shape* s) {
   if (waves > kWaves) waves = kWaves;
   s->tile_waves = waves;
   s->tile_lds_bytes = per_wave * waves;
+  s->wide_region = s->tile_layer_floats * s->L;
+  s->wide_floats = wide_layer_floats(*s) * s->L;
   return CNF_OK;
 }
 
 int tile_run(const Shape& s, const void* prepared, const float* in, float* out, float* ld,
              float* all, int64_t B, bool inverse, hipStream_t st) {
   if (B == 0) return CNF_OK;
+  if (!all && s.wide_floats > 0 && wide_ok(s))
+    return wide_run(s, prepared, in, out, ld, B, inverse, st);
   TileArgs a = make_args(s);
   const char* base = static_cast<const char*>(prepared);
   const int32_t* fwd_q = reinterpret_cast<const int32_t*>(base);
@@ -435,6 +439,7 @@ int prepare_run(const Shape& s, const float* const* params, void* prepared, hipS
       return CNF_ERR_HIP;
     }
   }
+  if (tiled && s.wide_floats > 0) return wide_prepare(s, params, prepared, st);
   return CNF_OK;
 }
 

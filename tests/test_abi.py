@@ -61,7 +61,7 @@ def test_kernel_family_selection():
     assert name(_lib.make_desc(3, 2, [5, 5], scale=0)) == "sgpr-fused"
     assert name(_lib.make_desc(10, 6, [5, 5], strict_nan=1)) == "valu-fused"
     assert name(_lib.make_desc(10, 6, [10, 10])) == "valu-fused"
-    assert name(_lib.make_desc(100, 12, [100, 100])) == "mfma-tile"
+    assert name(_lib.make_desc(100, 12, [100, 100])) == "mfma-wide"
     assert name(_lib.make_desc(10, 3, [4, 6, 3])) == "mfma-tile"
 
 

@@ -211,3 +211,34 @@ def test_fused_forward_loss_matches_oracle(kind):
         assert np.all(np.abs(got - ref) <= 1e-5 * (np.abs(ref) + B)), (got, ref)
         t2, _, _ = stack.forward_loss(x, y, kind=kind, det=0.5)
         assert torch.equal(terms, t2), "non-deterministic reduction"
+
+
+@pytest.mark.parametrize("D,L,hidden,flip,scale", [
+    (100, 12, [100, 100], True, True),   # cfg4 shape with random_flip permutations
+    (100, 4, [100], False, True),        # one hidden layer
+    (100, 3, [], False, False),          # NICE, no hidden layer
+    (32, 4, [64, 64], True, True),       # mid width, one partial state tile
+])
+def test_wide_kernel_matches_oracle_and_tile(D, L, hidden, flip, scale, monkeypatch):
+    """k_wide (cnf_wide.hip): register-resident MFMA path against the numpy
+    oracle, the round trip, and the LDS-tile kernel it replaces."""
+    flow = _make_flow(D, L, hidden, 0.05, 21, random_flip=flip, scale=scale)
+    assert flow._native_stack().kernel_name() == "mfma-wide"
+    x = _logits(1000, D, 3)                     # ragged: 31 full waves + 8 rows
+    with torch.no_grad():
+        z, ld = flow.transform(x)
+        xr, ild = flow.inverse_transform(z)
+    ol = _oracle_layers(flow)
+    if flip:
+        for l, ly in enumerate(flow.layers):
+            ol[l] = O.OracleLayer(D, ol[l].s_net, ol[l].t_net, ly.perm.reshape(-1).cpu().numpy())
+    ozs, old = O.flow_forward(ol, x.cpu().numpy())
+    assert rel_err(z.cpu().numpy(), ozs[-1]) <= TOL
+    assert rel_err(ld.cpu().numpy(), old) <= TOL
+    assert ((xr - x).abs() / (x.abs() + 1)).max().item() <= TOL
+    assert ((ild + ld).abs() / (ld.abs() + 1)).max().item() <= TOL
+    monkeypatch.setenv("CNF_WIDE", "0")          # the k_tile path, same prepared blob
+    with torch.no_grad():
+        zt, ldt = flow.transform(x)
+    assert rel_err(z.cpu().numpy(), zt.cpu().numpy()) <= TOL
+    assert rel_err(ld.cpu().numpy(), ldt.cpu().numpy()) <= TOL
