@@ -42,7 +42,7 @@ WORKLOADS = {
     # name: (D, L, hidden, B per GPU, inverse)
     "cfg1": dict(D=3, L=2, hidden=[5, 5], B=4096, scale=False, inverse=False),
     "cfg2": dict(D=10, L=6, hidden=[5, 5], B=1 << 20, scale=True, inverse=False),
-    "cfg4": dict(D=100, L=12, hidden=[100, 100], B=1 << 16, scale=True, inverse=False),
+    "cfg4": dict(D=100, L=12, hidden=[100, 100], B=1 << 18, scale=True, inverse=False),
     "cfg5": dict(D=10, L=6, hidden=[5, 5], B=1 << 20, scale=True, inverse=True),
 }
 
@@ -128,7 +128,8 @@ class Runner:
         self.i = 0
 
     def kernel_symbol(self):
-        return {"valu-fused": "k_valu", "sgpr-fused": "k_sgpr", "mfma-tile": "k_tile"}.get(
+        return {"valu-fused": "k_valu", "sgpr-fused": "k_sgpr", "mfma-tile": "k_tile",
+                "mfma-wide": "k_wide"}.get(
             self.stack.kernel_name(), self.stack.kernel_name())
 
     def step(self):

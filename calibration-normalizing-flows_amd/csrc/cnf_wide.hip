@@ -37,6 +37,16 @@ namespace {
 
 typedef float v16 __attribute__((ext_vector_type(16)));
 
+#ifndef CNF_WIDE_SB
+#define CNF_WIDE_SB 0  // sched_barrier mask: what may cross a K-step boundary
+#endif
+#ifndef CNF_WIDE_WPE
+#define CNF_WIDE_WPE 1  // waves per SIMD (1: 512 registers, the ring stays in flight)
+#endif
+#ifndef CNF_WIDE_P
+#define CNF_WIDE_P 16  // A-operand prefetch depth (K-steps in flight)
+#endif
+
 constexpr int kWRows = 32;  // rows per wave
 constexpr int kWWaves = 4;  // waves per block
 
@@ -109,6 +119,9 @@ __device__ __forceinline__ void kstep(v16& acc, float (&ring)[P], const float* _
   if constexpr (C < 0) bv = ones;
   else bv = in[C >> 4][C & 15];
   acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+  // keep each refill where it is: left alone, the scheduler sinks the loads
+  // next to their use (register pressure) and every MFMA waits vmcnt(0)
+  __builtin_amdgcn_sched_barrier(CNF_WIDE_SB);
 }
 
 template <class G, int I, int MT, bool RELU, int P, int TIN, int TOUT, int... N>
@@ -138,7 +151,7 @@ template <class G, int I, bool RELU, int TIN, int TOUT>
 __device__ __forceinline__ void lin(const float* __restrict__ A, const v16 (&in)[TIN],
                                     v16 (&out)[TOUT], float ones, int lane) {
   constexpr int NT = G::nks(I) * G::tout(I);
-  constexpr int P = NT < 12 ? NT : 12;
+  constexpr int P = NT < CNF_WIDE_P ? NT : CNF_WIDE_P;
   const float* __restrict__ a = A + lane;
   float ring[P];
 #pragma unroll
@@ -196,7 +209,7 @@ __device__ __forceinline__ void relayout(float* st, int* qs, int S, const int32_
 }
 
 template <int D, int H1, int H2, bool INV, int NETS>
-__global__ __launch_bounds__(64 * kWWaves, 2) void k_wide(
+__global__ __launch_bounds__(64 * kWWaves, CNF_WIDE_WPE) void k_wide(
     const float* __restrict__ W, const int32_t* __restrict__ qtab,
     const float* __restrict__ in, float* __restrict__ out, float* __restrict__ ld_out,
     int64_t B, int L) {
