@@ -43,9 +43,6 @@ typedef float v16 __attribute__((ext_vector_type(16)));
 #ifndef CNF_WIDE_WPE
 #define CNF_WIDE_WPE 1  // waves per SIMD (1: 512 registers, the ring stays in flight)
 #endif
-#ifndef CNF_WIDE_P
-#define CNF_WIDE_P 16  // A-operand prefetch depth (K-steps in flight)
-#endif
 
 constexpr int kWRows = 32;  // rows per wave
 constexpr int kWWaves = 4;  // waves per block
@@ -93,12 +90,18 @@ struct WG {
   static constexpr int NF = lin_off(NL);  // floats per net
   static constexpr int TS = tout(NL - 1);  // s / t tiles
   static constexpr int TH1 = H1 > 0 ? (H1 + 31) / 32 : 1, TH2 = H2 > 0 ? (H2 + 31) / 32 : 1;
-  static constexpr int mfmas() {  // per net
-    int n = 0;
-    for (int i = 0; i < NL; ++i) n += tout(i) * nks(i);
-    return n;
-  }
+  static constexpr int sbefore(int i) { return i == 0 ? 0 : sbefore(i - 1) + tout(i - 1) * nks(i - 1); }
+  static constexpr int mfmas() { return sbefore(NL); }  // K-steps (= MFMAs) per net
 };
+
+// A-operand ring depth for a layer of LS K-steps: the ring runs on across
+// layers (the next layer's first steps are fetched during this layer's last),
+// so its depth must divide LS; the deepest divisor in [6, 32].
+__host__ __device__ constexpr int ring_depth(int ls) {
+  for (int p = 32; p >= 6; --p)
+    if (ls % p == 0) return p;
+  return 1;
+}
 
 __device__ __forceinline__ void wsync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -106,30 +109,35 @@ __device__ __forceinline__ void wsync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// K-step N of M-tile MT of Linear I: A from the prefetch ring (refilled P
-// steps ahead), B from the input tile register the step names.
-template <class G, int I, int MT, int N, int P, int TIN>
+// K-step N of M-tile MT of Linear I of net NET: A from the prefetch ring,
+// which is refilled P steps ahead along the layer's flat A stream (both nets,
+// every Linear, 64 floats per step) and on into the next layer's (wn).
+template <class G, int NETS, int NET, int I, int MT, int N, int P, int TIN>
 __device__ __forceinline__ void kstep(v16& acc, float (&ring)[P], const float* __restrict__ a,
-                                      const v16 (&in)[TIN], float ones) {
-  constexpr int NK = G::nks(I), NT = NK * G::tout(I), T = MT * NK + N;
+                                      const float* __restrict__ an, const v16 (&in)[TIN],
+                                      float ones) {
+  constexpr int LS = NETS * G::mfmas();
+  constexpr int T = NET * G::mfmas() + G::sbefore(I) + MT * G::nks(I) + N;
   const float av = ring[T % P];
-  if constexpr (T + P < NT) ring[T % P] = a[(T + P) * 64];
+  if constexpr (T + P < LS) ring[T % P] = a[(T + P) * 64];
+  else ring[T % P] = an[(T + P - LS) * 64];
   constexpr int C = G::code(I, N);
   float bv;
   if constexpr (C < 0) bv = ones;
   else bv = in[C >> 4][C & 15];
   acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
   // keep each refill where it is: left alone, the scheduler sinks the loads
-  // next to their use (register pressure) and every MFMA waits vmcnt(0)
+  // next to their use and every MFMA waits vmcnt(0)
   __builtin_amdgcn_sched_barrier(CNF_WIDE_SB);
 }
 
-template <class G, int I, int MT, bool RELU, int P, int TIN, int TOUT, int... N>
+template <class G, int NETS, int NET, int I, int MT, bool RELU, int P, int TIN, int TOUT, int... N>
 __device__ __forceinline__ void mtile(float (&ring)[P], const float* __restrict__ a,
-                                      const v16 (&in)[TIN], v16 (&out)[TOUT], float ones,
+                                      const float* __restrict__ an, const v16 (&in)[TIN],
+                                      v16 (&out)[TOUT], float ones,
                                       std::integer_sequence<int, N...>) {
   v16 acc = {};
-  (kstep<G, I, MT, N, P>(acc, ring, a, in, ones), ...);
+  (kstep<G, NETS, NET, I, MT, N, P>(acc, ring, a, an, in, ones), ...);
   if constexpr (RELU) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = fmaxf(acc[r], 0.f);
@@ -137,43 +145,36 @@ __device__ __forceinline__ void mtile(float (&ring)[P], const float* __restrict_
   out[MT] = acc;
 }
 
-template <class G, int I, bool RELU, int P, int TIN, int TOUT, int... M>
-__device__ __forceinline__ void mtiles(float (&ring)[P], const float* __restrict__ a,
-                                       const v16 (&in)[TIN], v16 (&out)[TOUT], float ones,
-                                       std::integer_sequence<int, M...>) {
-  (mtile<G, I, M, RELU>(ring, a, in, out, ones,
-                        std::make_integer_sequence<int, G::nks(I)>{}), ...);
+template <class G, int NETS, int NET, int I, bool RELU, int P, int TIN, int TOUT, int... M>
+__device__ __forceinline__ void lin(float (&ring)[P], const float* __restrict__ a,
+                                    const float* __restrict__ an, const v16 (&in)[TIN],
+                                    v16 (&out)[TOUT], float ones,
+                                    std::integer_sequence<int, M...>) {
+  (mtile<G, NETS, NET, I, M, RELU>(ring, a, an, in, out, ones,
+                                   std::make_integer_sequence<int, G::nks(I)>{}), ...);
 }
 
-// One Linear: OUT[mt] = act(W . IN) over the geometry's M-tiles; the A tiles
-// (lane-ordered 256 B per K-step) stream through a register ring of P.
-template <class G, int I, bool RELU, int TIN, int TOUT>
-__device__ __forceinline__ void lin(const float* __restrict__ A, const v16 (&in)[TIN],
-                                    v16 (&out)[TOUT], float ones, int lane) {
-  constexpr int NT = G::nks(I) * G::tout(I);
-  constexpr int P = NT < CNF_WIDE_P ? NT : CNF_WIDE_P;
-  const float* __restrict__ a = A + lane;
-  float ring[P];
-#pragma unroll
-  for (int j = 0; j < P; ++j) ring[j] = a[j * 64];
-  mtiles<G, I, RELU>(ring, a, in, out, ones, std::make_integer_sequence<int, G::tout(I)>{});
-}
-
-// One conditioner MLP on the state X -> OUT (TS tiles over slots [0, DT)).
-template <class G>
-__device__ __forceinline__ void net(const float* __restrict__ w, const v16 (&X)[G::TX],
-                                    v16 (&OUT)[G::TS], float ones, int lane) {
+// One conditioner MLP (net NET of the layer) on the state X -> OUT (TS tiles
+// over slots [0, DT)); a / an: this layer's and the next layer's A streams.
+template <class G, int NETS, int NET, int P>
+__device__ __forceinline__ void net(float (&ring)[P], const float* __restrict__ a,
+                                    const float* __restrict__ an, const v16 (&X)[G::TX],
+                                    v16 (&OUT)[G::TS], float ones) {
+  using MS0 = std::make_integer_sequence<int, G::tout(0)>;
   if constexpr (G::NL == 1) {
-    lin<G, 0, false>(w, X, OUT, ones, lane);
+    lin<G, NETS, NET, 0, false>(ring, a, an, X, OUT, ones, MS0{});
   } else if constexpr (G::NL == 2) {
     v16 h1[G::TH1];
-    lin<G, 0, true>(w, X, h1, ones, lane);
-    lin<G, 1, false>(w + G::lin_off(1), h1, OUT, ones, lane);
+    lin<G, NETS, NET, 0, true>(ring, a, an, X, h1, ones, MS0{});
+    lin<G, NETS, NET, 1, false>(ring, a, an, h1, OUT, ones,
+                                std::make_integer_sequence<int, G::tout(1)>{});
   } else {
     v16 h1[G::TH1], h2[G::TH2];
-    lin<G, 0, true>(w, X, h1, ones, lane);
-    lin<G, 1, true>(w + G::lin_off(1), h1, h2, ones, lane);
-    lin<G, 2, false>(w + G::lin_off(2), h2, OUT, ones, lane);
+    lin<G, NETS, NET, 0, true>(ring, a, an, X, h1, ones, MS0{});
+    lin<G, NETS, NET, 1, true>(ring, a, an, h1, h2, ones,
+                               std::make_integer_sequence<int, G::tout(1)>{});
+    lin<G, NETS, NET, 2, false>(ring, a, an, h2, OUT, ones,
+                                std::make_integer_sequence<int, G::tout(2)>{});
   }
 }
 
@@ -245,18 +246,28 @@ __global__ __launch_bounds__(64 * kWWaves, CNF_WIDE_WPE) void k_wide(
   }
   wsync();
 
+  // the A stream: one ring for the whole launch, P K-steps ahead of the MFMAs
+  constexpr int P = ring_depth(NETS * G::mfmas());
+  float ring[P];
+  {
+    const float* a0 = W + (int64_t)(INV ? L - 1 : 0) * NETS * G::NF + lane;
+#pragma unroll
+    for (int j = 0; j < P; ++j) ring[j] = a0[j * 64];
+  }
   float ld = 0.f;
   for (int stp = 0; stp < L; ++stp) {
     const int l = INV ? L - 1 - stp : stp;
+    const int ln = stp + 1 < L ? (INV ? l - 1 : l + 1) : l;  // last layer: harmless re-read
     const int32_t* __restrict__ q = qtab + l * D;
     if constexpr (INV) relayout<D, TX>(st, qs, S, q, X, lane);  // flip / rev_perm first
-    const float* __restrict__ wl = W + (int64_t)l * NETS * G::NF;
+    const float* __restrict__ wl = W + (int64_t)l * NETS * G::NF + lane;
+    const float* __restrict__ wn = W + (int64_t)ln * NETS * G::NF + lane;
     v16 Sv[TS], Tv[TS];
     if constexpr (NETS == 2) {
-      net<G>(wl, X, Sv, ones, lane);
-      net<G>(wl + G::NF, X, Tv, ones, lane);
+      net<G, 2, 0>(ring, wl, wn, X, Sv, ones);
+      net<G, 2, 1>(ring, wl, wn, X, Tv, ones);
     } else {
-      net<G>(wl, X, Tv, ones, lane);
+      net<G, 1, 0>(ring, wl, wn, X, Tv, ones);
     }
 #pragma unroll
     for (int mt = 0; mt < TS; ++mt)
@@ -266,7 +277,9 @@ __global__ __launch_bounds__(64 * kWWaves, CNF_WIDE_WPE) void k_wide(
         float x = X[mt][r];
         if constexpr (NETS == 2) {
           const float s = Sv[mt][r];
-          x = INV ? (x - Tv[mt][r]) * expf(-s) : fmaf(x, expf(s), Tv[mt][r]);
+          // exp(s) = 2^(s log2 e): one v_exp_f32 (|rel err| < 1e-6 for |s| < 10)
+          const float e = __builtin_amdgcn_exp2f((INV ? -s : s) * 1.4426950408889634f);
+          x = INV ? (x - Tv[mt][r]) * e : fmaf(x, e, Tv[mt][r]);
           ld += INV ? -s : s;
         } else {
           x = INV ? x - Tv[mt][r] : x + Tv[mt][r];
