@@ -41,7 +41,10 @@ typedef float v16 __attribute__((ext_vector_type(16)));
 #define CNF_WIDE_SB 0  // sched_barrier mask: what may cross a K-step boundary
 #endif
 #ifndef CNF_WIDE_WPE
-#define CNF_WIDE_WPE 1  // waves per SIMD (1: 512 registers, the ring stays in flight)
+#define CNF_WIDE_WPE 2  // waves per SIMD
+#endif
+#ifndef CNF_WIDE_PMAX
+#define CNF_WIDE_PMAX (CNF_WIDE_WPE == 1 ? 32 : 16)  // deepest A-operand ring
 #endif
 
 constexpr int kWRows = 32;  // rows per wave
@@ -96,9 +99,9 @@ struct WG {
 
 // A-operand ring depth for a layer of LS K-steps: the ring runs on across
 // layers (the next layer's first steps are fetched during this layer's last),
-// so its depth must divide LS; the deepest divisor in [6, 32].
-__host__ __device__ constexpr int ring_depth(int ls) {
-  for (int p = 32; p >= 6; --p)
+// so its depth must divide LS; the deepest divisor in [6, pmax].
+__host__ __device__ constexpr int ring_depth(int ls, int pmax) {
+  for (int p = pmax; p >= 6; --p)
     if (ls % p == 0) return p;
   return 1;
 }
@@ -131,50 +134,81 @@ __device__ __forceinline__ void kstep(v16& acc, float (&ring)[P], const float* _
   __builtin_amdgcn_sched_barrier(CNF_WIDE_SB);
 }
 
-template <class G, int NETS, int NET, int I, int MT, bool RELU, int P, int TIN, int TOUT, int... N>
+// Epilogues of an M-tile's accumulator: store (hidden layers with ReLU, or
+// the t-net's output) or the fused affine update of the state (the s-net's
+// last Linear, run after the t-net: each s tile is applied and dropped, so s
+// and t are never live together).
+template <bool RELU, int TOUT>
+struct EpOut {
+  v16 (&o)[TOUT];
+  template <int MT>
+  __device__ __forceinline__ void put(v16 acc) {
+    if constexpr (RELU) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = fmaxf(acc[r], 0.f);
+    }
+    o[MT] = acc;
+  }
+};
+
+template <bool INV, int TX, int TS>
+struct EpAffine {
+  v16 (&X)[TX];
+  const v16 (&T)[TS];
+  float& ld;
+  template <int MT>
+  __device__ __forceinline__ void put(v16 s) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      // slots >= DT of these tiles got s = t = 0 (zero A rows and bias): x stays x
+      // exp(s) = 2^(s log2 e): one v_exp_f32 (|rel err| < 1e-6 for |s| < 10)
+      const float e = __builtin_amdgcn_exp2f((INV ? -s[r] : s[r]) * 1.4426950408889634f);
+      const float x = X[MT][r];
+      X[MT][r] = INV ? (x - T[MT][r]) * e : fmaf(x, e, T[MT][r]);
+      ld += INV ? -s[r] : s[r];
+    }
+  }
+};
+
+template <class G, int NETS, int NET, int I, int MT, int P, int TIN, class EP, int... N>
 __device__ __forceinline__ void mtile(float (&ring)[P], const float* __restrict__ a,
                                       const float* __restrict__ an, const v16 (&in)[TIN],
-                                      v16 (&out)[TOUT], float ones,
-                                      std::integer_sequence<int, N...>) {
+                                      EP& ep, float ones, std::integer_sequence<int, N...>) {
   v16 acc = {};
   (kstep<G, NETS, NET, I, MT, N, P>(acc, ring, a, an, in, ones), ...);
-  if constexpr (RELU) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = fmaxf(acc[r], 0.f);
-  }
-  out[MT] = acc;
+  ep.template put<MT>(acc);
 }
 
-template <class G, int NETS, int NET, int I, bool RELU, int P, int TIN, int TOUT, int... M>
+template <class G, int NETS, int NET, int I, int P, int TIN, class EP, int... M>
 __device__ __forceinline__ void lin(float (&ring)[P], const float* __restrict__ a,
                                     const float* __restrict__ an, const v16 (&in)[TIN],
-                                    v16 (&out)[TOUT], float ones,
-                                    std::integer_sequence<int, M...>) {
-  (mtile<G, NETS, NET, I, M, RELU>(ring, a, an, in, out, ones,
-                                   std::make_integer_sequence<int, G::nks(I)>{}), ...);
+                                    EP& ep, float ones, std::integer_sequence<int, M...>) {
+  (mtile<G, NETS, NET, I, M>(ring, a, an, in, ep, ones,
+                             std::make_integer_sequence<int, G::nks(I)>{}), ...);
 }
 
-// One conditioner MLP (net NET of the layer) on the state X -> OUT (TS tiles
-// over slots [0, DT)); a / an: this layer's and the next layer's A streams.
-template <class G, int NETS, int NET, int P>
+// One conditioner MLP (stream position NET of the layer) on the state X; its
+// last Linear's tiles go to ep.  a / an: this layer's and the next layer's A
+// streams.
+template <class G, int NETS, int NET, int P, class EP>
 __device__ __forceinline__ void net(float (&ring)[P], const float* __restrict__ a,
-                                    const float* __restrict__ an, const v16 (&X)[G::TX],
-                                    v16 (&OUT)[G::TS], float ones) {
+                                    const float* __restrict__ an, const v16 (&X)[G::TX], EP& ep,
+                                    float ones) {
   using MS0 = std::make_integer_sequence<int, G::tout(0)>;
   if constexpr (G::NL == 1) {
-    lin<G, NETS, NET, 0, false>(ring, a, an, X, OUT, ones, MS0{});
+    lin<G, NETS, NET, 0>(ring, a, an, X, ep, ones, MS0{});
   } else if constexpr (G::NL == 2) {
     v16 h1[G::TH1];
-    lin<G, NETS, NET, 0, true>(ring, a, an, X, h1, ones, MS0{});
-    lin<G, NETS, NET, 1, false>(ring, a, an, h1, OUT, ones,
-                                std::make_integer_sequence<int, G::tout(1)>{});
+    EpOut<true, G::TH1> e1{h1};
+    lin<G, NETS, NET, 0>(ring, a, an, X, e1, ones, MS0{});
+    lin<G, NETS, NET, 1>(ring, a, an, h1, ep, ones, std::make_integer_sequence<int, G::tout(1)>{});
   } else {
     v16 h1[G::TH1], h2[G::TH2];
-    lin<G, NETS, NET, 0, true>(ring, a, an, X, h1, ones, MS0{});
-    lin<G, NETS, NET, 1, true>(ring, a, an, h1, h2, ones,
-                               std::make_integer_sequence<int, G::tout(1)>{});
-    lin<G, NETS, NET, 2, false>(ring, a, an, h2, OUT, ones,
-                                std::make_integer_sequence<int, G::tout(2)>{});
+    EpOut<true, G::TH1> e1{h1};
+    EpOut<true, G::TH2> e2{h2};
+    lin<G, NETS, NET, 0>(ring, a, an, X, e1, ones, MS0{});
+    lin<G, NETS, NET, 1>(ring, a, an, h1, e2, ones, std::make_integer_sequence<int, G::tout(1)>{});
+    lin<G, NETS, NET, 2>(ring, a, an, h2, ep, ones, std::make_integer_sequence<int, G::tout(2)>{});
   }
 }
 
@@ -247,7 +281,7 @@ __global__ __launch_bounds__(64 * kWWaves, CNF_WIDE_WPE) void k_wide(
   wsync();
 
   // the A stream: one ring for the whole launch, P K-steps ahead of the MFMAs
-  constexpr int P = ring_depth(NETS * G::mfmas());
+  constexpr int P = ring_depth(NETS * G::mfmas(), CNF_WIDE_PMAX);
   float ring[P];
   {
     const float* a0 = W + (int64_t)(INV ? L - 1 : 0) * NETS * G::NF + lane;
@@ -262,30 +296,19 @@ __global__ __launch_bounds__(64 * kWWaves, CNF_WIDE_WPE) void k_wide(
     if constexpr (INV) relayout<D, TX>(st, qs, S, q, X, lane);  // flip / rev_perm first
     const float* __restrict__ wl = W + (int64_t)l * NETS * G::NF + lane;
     const float* __restrict__ wn = W + (int64_t)ln * NETS * G::NF + lane;
-    v16 Sv[TS], Tv[TS];
-    if constexpr (NETS == 2) {
-      net<G, 2, 0>(ring, wl, wn, X, Sv, ones);
-      net<G, 2, 1>(ring, wl, wn, X, Tv, ones);
+    v16 Tv[TS];
+    EpOut<false, TS> et{Tv};
+    if constexpr (NETS == 2) {  // stream order (cnf_prepare): t-net, then s-net
+      net<G, 2, 0>(ring, wl, wn, X, et, ones);
+      EpAffine<INV, TX, TS> ea{X, Tv, ld};
+      net<G, 2, 1>(ring, wl, wn, X, ea, ones);
     } else {
-      net<G, 1, 0>(ring, wl, wn, X, Tv, ones);
+      net<G, 1, 0>(ring, wl, wn, X, et, ones);
+#pragma unroll
+      for (int mt = 0; mt < TS; ++mt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) X[mt][r] = INV ? X[mt][r] - Tv[mt][r] : X[mt][r] + Tv[mt][r];
     }
-#pragma unroll
-    for (int mt = 0; mt < TS; ++mt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        // slots >= DT of these tiles got s = t = 0 (zero A rows and bias): x stays x
-        float x = X[mt][r];
-        if constexpr (NETS == 2) {
-          const float s = Sv[mt][r];
-          // exp(s) = 2^(s log2 e): one v_exp_f32 (|rel err| < 1e-6 for |s| < 10)
-          const float e = __builtin_amdgcn_exp2f((INV ? -s : s) * 1.4426950408889634f);
-          x = INV ? (x - Tv[mt][r]) * e : fmaf(x, e, Tv[mt][r]);
-          ld += INV ? -s : s;
-        } else {
-          x = INV ? x - Tv[mt][r] : x + Tv[mt][r];
-        }
-        X[mt][r] = x;
-      }
     if constexpr (!INV) relayout<D, TX>(st, qs, S, q, X, lane);  // perm then flip
   }
 
@@ -434,7 +457,10 @@ int wide_prepare(const Shape& s, const float* const* params, void* prepared, hip
         g.nin_full = s.units[i];
         g.nout_full = s.units[i + 1];
         e->fill(i, &g);
-        g.dst = ((int64_t)l * s.nets + net) * e->net_floats + e->lin_off[i];
+        // stream order: the t-net first (its output must be live when the s-net's
+        // last Linear applies the affine update tile by tile)
+        const int pos = s.nets == 2 ? 1 - net : net;
+        g.dst = ((int64_t)l * s.nets + pos) * e->net_floats + e->lin_off[i];
       }
     }
     hipLaunchKernelGGL(k_prepare_wide, dim3(a.nseg), dim3(256), 0, st, a, region);
