@@ -372,10 +372,9 @@ struct SEntry {
   KFn fn[3][2][2];  // [pipe][nets - 1][inverse]
 };
 
-// (the inverse never takes the LDS-DMA form, see sgpr_run)
 #define CNF_SGPR_P(D, H1, H2, P)                                                      \
-  {{k_sgpr<D, H1, H2, false, 1, kRW, kRows, P>, k_sgpr<D, H1, H2, true, 1, kRW, kRows, 0>}, \
-   {k_sgpr<D, H1, H2, false, 2, kRW, kRows, P>, k_sgpr<D, H1, H2, true, 2, kRW, kRows, 0>}}
+  {{k_sgpr<D, H1, H2, false, 1, kRW, kRows, P>, k_sgpr<D, H1, H2, true, 1, kRW, kRows, P>}, \
+   {k_sgpr<D, H1, H2, false, 2, kRW, kRows, P>, k_sgpr<D, H1, H2, true, 2, kRW, kRows, P>}}
 #define CNF_SGPR(D, H1, H2) \
   {D, H1, H2, {CNF_SGPR_P(D, H1, H2, 0), CNF_SGPR_P(D, H1, H2, 1), CNF_SGPR_P(D, H1, H2, 2)}}
 
@@ -452,12 +451,11 @@ static KFn pick(const SEntry* e, const Shape& s, bool inverse, bool pipe) {
   return e->fn[pipe ? pipe_mode() : 0][s.scale ? 1 : 0][inverse ? 1 : 0];
 }
 
-int64_t sgpr_blocks(const Shape& s, int64_t B) {
+static int64_t blocks_dir(const Shape& s, int64_t B, bool inverse) {
   const int64_t ntiles = (B + kRW * kRows - 1) / (kRW * kRows);
   const SEntry* e = find(s);
   if (!e || !pipe_on()) return ntiles;
-  // the grid does not depend on the direction: both directions share one table row
-  int cap = resident(pick(e, s, false, true), lds_bytes(s, true));
+  int cap = resident(pick(e, s, inverse, true), lds_bytes(s, true));
   if (const char* g = std::getenv("CNF_SGPR_GRID")) {  // experiment: fixed grid cap
     const int n = std::atoi(g);
     if (n > 0) cap = n;
@@ -472,6 +470,8 @@ int64_t sgpr_blocks(const Shape& s, int64_t B) {
   return (ntiles + per - 1) / per;
 }
 
+int64_t sgpr_blocks(const Shape& s, int64_t B) { return blocks_dir(s, B, false); }
+
 int sgpr_run(const Shape& s, const void* prepared, const float* in, float* out, float* ld,
              float* all, int64_t B, bool inverse, hipStream_t st, const int64_t* y,
              float* loss_ws, int kind, float det, float* loss_terms) {
@@ -485,11 +485,13 @@ int sgpr_run(const Shape& s, const void* prepared, const float* in, float* out, 
   const float* W = reinterpret_cast<const float*>(base + idx_bytes(s)) + s.sp_region;
   auto al = [](const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   const int vec = al(in) && al(out) && al(all);
-  // the inverse keeps one tile per block: its LDS-DMA form needs more VGPRs
-  // than the 5-wave bound allows (measured: scratch spills, 2x slower)
-  const bool pipe = pipe_on() && !inverse;
+  // the inverse takes the persistent LDS-DMA form too since the weight loads became
+  // compiler-visible (118 VGPRs, 4 waves/SIMD, no spills): -8 % on cfg5.
+  // A/B switch CNF_SGPR_INV_PIPE=0 keeps one tile per block.
+  const char* ip = std::getenv("CNF_SGPR_INV_PIPE");
+  const bool pipe = pipe_on() && (!inverse || !(ip && ip[0] == '0'));
   KFn fn = pick(e, s, inverse, pipe);
-  const int64_t nblk = pipe ? sgpr_blocks(s, B) : (B + kRW * kRows - 1) / (kRW * kRows);
+  const int64_t nblk = pipe ? blocks_dir(s, B, inverse) : (B + kRW * kRows - 1) / (kRW * kRows);
   const size_t lds = lds_bytes(s, pipe);
   // one-launch loss hand-off on the persistent grid (workspace ticket word,
   // zeroed by the caller once; the last block resets it)
