@@ -62,6 +62,30 @@ def algo_bytes_per_vec(D, L, all_outputs=False, labels=False):
     return 4 * D + 4 * D * (L if all_outputs else 1) + 4 + (8 if labels else 0)
 
 
+def roofline(B, bytes_vec, flops_vec, seconds, mfma=False):
+    """Roofline of one launch over B vectors: the attainable rate
+    is min(HBM peak / bytes, compute peak / flops); `bound` names the roof that
+    binds first and `frac` = achieved rate / attainable rate.  Compute is fp32
+    VALU (packed FMA) for the narrow flows, fp32 MFMA for the wide ones."""
+    comp_peak = MFMA_F32_PEAK_TFLOPS if mfma else VALU_PEAK_TFLOPS
+    hbm_rate = HBM_PEAK_GBS * 1e9 / bytes_vec          # vectors/s if HBM-bound
+    comp_rate = comp_peak * 1e12 / flops_vec           # vectors/s if compute-bound
+    rate = B / seconds
+    gbs = B * bytes_vec / seconds / 1e9
+    tfs = B * flops_vec / seconds / 1e12
+    if comp_rate <= hbm_rate:
+        r = {"bound": "mfma" if mfma else "valu", "achieved": round(tfs, 2),
+             "peak": comp_peak, "unit": "TFLOP/s"}
+    else:
+        r = {"bound": "hbm", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s"}
+    r["frac"] = round(rate / min(hbm_rate, comp_rate), 4)
+    r["hbm_gbs"] = round(gbs, 2)
+    r["hbm_frac"] = round(gbs / HBM_PEAK_GBS, 4)
+    r["compute_tflops"] = round(tfs, 2)
+    r["compute_frac"] = round(tfs / comp_peak, 4)
+    return r
+
+
 def make_flow(w, device, seed=0):
     from flows.flows import Flow, NvpCouplingLayer
     torch.manual_seed(seed)
@@ -229,7 +253,7 @@ def cpu_baseline(w, seconds=10.0):
     flow = make_flow(w, "cpu")
     st = {k: v for k, v in flow.state_dict().items()}
     layers = P.layers_from_state(st, w["L"], len(w["hidden"]) + 1, w["scale"], True)
-    B = min(w["B"], 1 << 18)
+    B = w["B"]  # the config's own batch (2^20 for cfg2)
     x, _ = synthetic_logits(B, w["D"], "cpu", 99)
     P.flow_forward(layers, x)
     times = []
@@ -240,10 +264,40 @@ def cpu_baseline(w, seconds=10.0):
         times.append(time.perf_counter() - t)
     rate = B / float(np.median(times))
     return {"value": rate, "unit": "logit-vectors/sec", "cores": torch.get_num_threads(),
-            "kind": "port",
-            "sample": "%d x %d-vector forward passes (B=%d, D=%d, L=%d, h=%s) with the "
-                      "op-for-op torch CPU port, median; port/reference time ratio 0.81-1.02 "
-                      "(profiles/r01_cpu_port_ratio.jsonl, DESIGN.md)" % (len(times), B, B, w["D"], w["L"], w["hidden"])}
+            "nproc": os.cpu_count(), "kind": "port",
+            "sample": "%d x %d-vector forward passes (the config's B, D=%d, L=%d, h=%s) with the "
+                      "op-for-op torch CPU port on %d torch threads of a %d-CPU host, median; "
+                      "port/reference time ratio: profiles/*_cpu_port_ratio.jsonl, DESIGN.md"
+                      % (len(times), B, w["D"], w["L"], w["hidden"], torch.get_num_threads(),
+                         os.cpu_count() or 0)}
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(n, argv):
+    """`bench.py --gpus N` without a launcher: start N fresh rank processes
+    (one per GPU, RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* in their env) as
+    children of this process, which never touches the GPU, and exit with the
+    worst child status.  torch.distributed.run sets WORLD_SIZE itself, so the
+    driver's launcher path never comes here."""
+    import subprocess
+    port = os.environ.get("MASTER_PORT") or str(free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rc = 0
+    for p in procs:
+        c = p.wait()
+        if c != 0 and rc == 0:
+            rc = c if c > 0 else 128 - c
+    return rc
 
 
 def main():
@@ -257,14 +311,32 @@ def main():
     ap.add_argument("--no-variants", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--launch-check", action="store_true",
+                    help="rank wiring only: gloo process group, no GPU (CPU test of the launcher)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        if not args.launch_check and torch.cuda.device_count() < args.gpus:
+            sys.exit("bench.py --gpus %d: only %d GPU(s) visible" % (args.gpus,
+                                                                   torch.cuda.device_count()))
+        sys.exit(self_launch(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.exit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    if args.launch_check:
+        dist.init_process_group("gloo", init_method="env://")
+        t = torch.tensor([float(rank)])
+        dist.all_reduce(t)
+        if rank == 0:
+            print(json.dumps({"n_gpus": dist.get_world_size(), "rank_sum": t.item()}))
+        dist.destroy_process_group()
+        return
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        assert dist.get_world_size() == args.gpus
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -293,25 +365,18 @@ def main():
     k_avg = kernel_only_seconds(runner, max(50, args.steps // 2))
     bytes_vec = algo_bytes_per_vec(w["D"], w["L"], labels=(mode == "loss"))
     flops_vec = algo_flops_per_vec(w["D"], w["L"], w["hidden"], w["scale"])
-    achieved_gbs = w["B"] * bytes_vec / k_avg / 1e9
-    achieved_tf = w["B"] * flops_vec / k_avg / 1e12
     mfma_bound = w["D"] >= 32
-    roof = {
-        "bound": "mfma" if mfma_bound else "hbm",
-        "achieved": round(achieved_tf if mfma_bound else achieved_gbs, 2),
-        "peak": MFMA_F32_PEAK_TFLOPS if mfma_bound else HBM_PEAK_GBS,
-        "unit": "TFLOP/s" if mfma_bound else "GB/s",
-        "frac": None, "traffic": None,
+    roof = roofline(w["B"], bytes_vec, flops_vec, k_avg, mfma=mfma_bound)
+    roof.update({
+        "traffic": None,
         "kernel": runner.stack.kernel_name(),
         "kernel_avg_us": round(k_avg * 1e6, 3),
-        "timed_kernels": ("%s + k_reduce_rows (block-order NLL sum): the whole cnf_forward_loss "
+        "timed_kernels": ("%s + k_reduce_rows4 (block-order NLL sum): the whole cnf_forward_loss "
                           "call, HIP events on its stream" % runner.kernel_symbol()) if mode == "loss"
                          else runner.kernel_symbol(),
         "algo_bytes_per_vec": bytes_vec, "algo_flops_per_vec": flops_vec,
-        "valu_tflops": round(achieved_tf, 2), "valu_frac": round(achieved_tf / VALU_PEAK_TFLOPS, 4),
         "rotating_sets": runner.nsets,
-    }
-    roof["frac"] = round(roof["achieved"] / roof["peak"], 4)
+    })
     tr = measured_traffic(args.workload, w["B"])
     if tr is not None:
         roof["traffic"] = tr["traffic_bytes_per_launch"]
@@ -328,10 +393,11 @@ def main():
             ka = kernel_only_seconds(r, 30)
             bv = algo_bytes_per_vec(wl["D"], wl["L"], allo)
             fv = algo_flops_per_vec(wl["D"], wl["L"], wl["hidden"], wl["scale"])
+            rf = roofline(wl["B"], bv, fv, ka, mfma=wl["D"] >= 32)
             variants[name] = {"vec_per_s": round(wl["B"] / ka, 1), "kernel_avg_us": round(ka * 1e6, 2),
                               "B": wl["B"], "kernel": r.stack.kernel_name(),
-                              "hbm_gbs": round(wl["B"] * bv / ka / 1e9, 1),
-                              "tflops": round(wl["B"] * fv / ka / 1e12, 2)}
+                              "hbm_gbs": rf["hbm_gbs"], "tflops": rf["compute_tflops"],
+                              "bound": rf["bound"], "frac": rf["frac"]}
             del r
             torch.cuda.empty_cache()
         variants["cfg2_train_step_fused_loss_vjp"] = train_step_rate(dev)

@@ -65,9 +65,10 @@ class DummyCalibrator(Calibrator):
         return softmax(logits, axis=1)
 
 
-def _native_stack(flow, dev):
+def _native_stack(flow, dev, need_vjp=True):
     """The fused CouplingStack behind `flow`, or None when the flow is not a
-    stack of NvpCouplingLayers or the device is not a ROCm GPU."""
+    stack of NvpCouplingLayers or the device is not a ROCm GPU (need_vjp: the
+    shape must also have a native reverse mode)."""
     if torch.device(dev).type != "cuda":
         return None
     try:
@@ -80,6 +81,8 @@ def _native_stack(flow, dev):
     if flow._strict():
         return None
     stack = flow._native_stack()
+    if not need_vjp:
+        return stack
     try:
         import ctypes
         n = ctypes.c_size_t()
@@ -105,6 +108,7 @@ class TorchFlowCalibrator(Calibrator):
         self.CE = nn.CrossEntropyLoss()
         self.optimizer = torch.optim.Adam(self.flow.parameters())
         self._replica = None
+        self._lp_dev = None
         self.history = self.fit(self.logits, self.target,
                                 epochs=kwargs.get('epochs', 1000),
                                 batch_size=kwargs.get('batch_size', logits.shape[0]))
@@ -206,6 +210,25 @@ class TorchFlowCalibrator(Calibrator):
             rep.eval()
             self._replica = (key, rep)
         return self._replica[1]
+
+    def predict(self, logits):
+        """Calibrator.predict (calibrators.py:40-44 with predict_post, :330-353):
+        centring, the flow, softmax and the prior correction
+        softmax(log(p + 1e-7) - log_priors).  On a ROCm device this is ONE fused
+        launch (cnf_predict) on a resident replica of the flow, with one H2D
+        copy of the logits and one D2H copy of the probabilities."""
+        if torch.device(self.dev).type == "cuda":
+            flow = self._device_flow()
+            stack = _native_stack(flow, self.dev, need_vjp=False)
+            if stack is not None:
+                x = torch.as_tensor(np.asarray(logits), dtype=torch.float).to(self.dev)
+                if self._lp_dev is None:
+                    self._lp_dev = torch.as_tensor(self.log_priors, dtype=torch.float,
+                                                   device=self.dev)
+                with torch.no_grad():
+                    probs = stack.predict(x, self._lp_dev)
+                return probs.cpu().numpy().astype(np.float64)
+        return super().predict(logits)
 
     def predict_logits(self, logits):
         logits = torch.as_tensor(logits, dtype=torch.float)

@@ -20,12 +20,14 @@ MAX_HIDDEN = 8
 MAX_DIM = 256
 LOSS_CAL = 0
 LOSS_CE = 1
+OPT_NO_SGPR = 1   # cnf_desc.options (include/cnf.h)
+OPT_NO_WIDE = 2
 
 # Every symbol include/cnf.h declares (checked by tests/test_abi.py).
 EXPORTS = (
     "cnf_param_count", "cnf_param_tensor_count", "cnf_prepared_bytes", "cnf_prepare",
     "cnf_forward", "cnf_inverse", "cnf_forward_loss_workspace_bytes", "cnf_forward_loss",
-    "cnf_vjp_workspace_bytes", "cnf_vjp", "cnf_loss_vjp",
+    "cnf_predict", "cnf_vjp_workspace_bytes", "cnf_vjp", "cnf_loss_vjp",
     "cnf_kernel_name", "cnf_strerror", "cnf_last_hip_error", "cnf_abi_version",
 )
 
@@ -41,7 +43,7 @@ class CnfDesc(ctypes.Structure):
         ("scale", ctypes.c_int32),
         ("shift", ctypes.c_int32),
         ("strict_nan", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("options", ctypes.c_int32),
         ("perms", ctypes.POINTER(ctypes.c_int64)),
     ]
 
@@ -77,6 +79,7 @@ def _bind(lib):
                                              [D, I64, ctypes.POINTER(ctypes.c_size_t)]),
         "cnf_forward_loss": (ctypes.c_int, [D, P, P, P, I32, F, P, P, P, I64, P, ctypes.c_size_t,
                                             P]),
+        "cnf_predict": (ctypes.c_int, [D, P, P, P, P, P, I64, P]),
         "cnf_vjp_workspace_bytes": (ctypes.c_int, [D, I64, ctypes.POINTER(ctypes.c_size_t)]),
         "cnf_vjp": (ctypes.c_int, [D, P, P, P, P, P, P, P, I64, P, ctypes.c_size_t, P]),
         "cnf_loss_vjp": (ctypes.c_int, [D, P, P, P, I32, F, F, P, P, P, I64, P, ctypes.c_size_t,
@@ -118,7 +121,8 @@ def check(fn, status):
         raise (UnsupportedShape if status == -3 else CnfError)(fn, status, l)
 
 
-def make_desc(dim, n_layers, hidden, scale=True, shift=True, strict_nan=False, perms=None):
+def make_desc(dim, n_layers, hidden, scale=True, shift=True, strict_nan=False, perms=None,
+              options=0):
     """Build a CnfDesc; `perms` is an int64 host tensor [L, D] (row[0] < 0: no perm)
     that must stay alive while the descriptor is used."""
     hidden = list(hidden)
@@ -134,6 +138,7 @@ def make_desc(dim, n_layers, hidden, scale=True, shift=True, strict_nan=False, p
     d.scale = int(bool(scale))
     d.shift = int(bool(shift))
     d.strict_nan = int(bool(strict_nan))
+    d.options = int(options)
     d.perms = None
     if perms is not None:
         assert perms.dtype == torch.int64 and perms.is_contiguous() and not perms.is_cuda

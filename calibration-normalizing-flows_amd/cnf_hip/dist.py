@@ -78,6 +78,9 @@ class ShardedFlowTrainer:
             with torch.no_grad():
                 for t in flow.state_dict().values():
                     dist.broadcast(t, src=0, group=group)
+            # collectives write in place without bumping version counters
+            if hasattr(flow, "invalidate_native"):
+                flow.invalidate_native()
 
     def step(self, x, y, global_batch, kind=_lib.LOSS_CAL, det=1.0):
         """One synchronous step on this rank's shard; returns the global

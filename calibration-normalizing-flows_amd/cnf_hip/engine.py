@@ -6,6 +6,14 @@ fused launch (cnf_forward / cnf_inverse / cnf_vjp in include/cnf.h).  All
 buffers are torch allocations on the input's device; the stream is
 `torch.cuda.current_stream()`, so launches order with surrounding torch work
 and can be captured into a CUDA(HIP) graph.
+
+Cache validity.  The prepared blob (weights re-laid out for the kernels, the
+flip / random_flip permutation folded into gather tables) is rebuilt whenever
+a parameter's or a permutation's storage or in-place version changes: optimizer
+steps, `load_state_dict` and `copy_` all bump `_version`.  Writes through
+`.data` do not (torch hides them from autograd too); after such a write call
+`Flow.invalidate_native()` (or `CouplingStack.invalidate()`).  A backward whose
+weights changed in place since its forward raises, as autograd does.
 """
 import ctypes
 
@@ -14,7 +22,7 @@ import torch
 from . import _lib
 
 # counts of native launches (tests assert the HIP path really ran)
-stats = {"forward": 0, "inverse": 0, "prepare": 0, "vjp": 0, "loss_vjp": 0}
+stats = {"forward": 0, "inverse": 0, "prepare": 0, "vjp": 0, "loss_vjp": 0, "predict": 0}
 
 
 def _ptr(t):
@@ -25,12 +33,16 @@ def _stream(device):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
+def _stream_key(device):
+    return (device, torch.cuda.current_stream(device).cuda_stream)
+
+
 class CouplingStack:
     """A fused stack of NvpCouplingLayers (flows/flows.py:68-126) sharing
     dim / hidden_size / scale / shift.  Layers keep owning their parameters;
     the stack only reads them (state_dict order) through cnf_prepare."""
 
-    def __init__(self, layers, strict_nan=False):
+    def __init__(self, layers, strict_nan=False, options=0):
         layers = list(layers)
         l0 = layers[0]
         self.layers = layers
@@ -39,18 +51,41 @@ class CouplingStack:
         self.scale = bool(l0.scale)
         self.shift = bool(l0.shift)
         self.strict_nan = bool(strict_nan)
+        self.options = int(options)
         self.L = len(layers)
+        self._perm_key = None
         self._perms = None
-        if any(ly.random_flip for ly in layers):
+        self._refresh_desc()
+        self._cache = {}
+        self._loss_ws = {}
+
+    # -- descriptor and permutations ----------------------------------------
+    def _perm_tensors(self):
+        return [ly.perm for ly in self.layers if ly.random_flip]
+
+    def _perm_state(self):
+        return tuple((p.data_ptr(), p._version) for p in self._perm_tensors())
+
+    def _refresh_desc(self):
+        """(Re)build the host permutation table and the descriptor from the
+        layers' current `perm` values (one small D2H copy, only on change)."""
+        self._perm_key = self._perm_state()
+        if any(ly.random_flip for ly in self.layers):
             p = torch.full((self.L, self.dim), -1, dtype=torch.int64)
-            for i, ly in enumerate(layers):
+            for i, ly in enumerate(self.layers):
                 if ly.random_flip:
                     p[i] = ly.perm.detach().reshape(-1).cpu()
             self._perms = p.contiguous()
+        else:
+            self._perms = None
         self.desc = _lib.make_desc(self.dim, self.L, self.hidden, self.scale, self.shift,
-                                   self.strict_nan, self._perms)
-        self._cache = {}
-        self._loss_ws = {}
+                                   self.strict_nan, self._perms, self.options)
+
+    def invalidate(self):
+        """Forget every prepared blob (after writes the version counters do
+        not see, e.g. through `.data`)."""
+        self._cache.clear()
+        self._perm_key = None
 
     @staticmethod
     def compatible(layers):
@@ -78,14 +113,22 @@ class CouplingStack:
                                                                   ctypes.byref(n)))
         return n.value
 
+    def state_key(self):
+        """Identity of everything the prepared blob encodes."""
+        return (tuple((p.data_ptr(), p._version) for p in self.param_tensors()),
+                self._perm_state())
+
     def prepared(self, device):
-        """Device blob for this stack, rebuilt only when a parameter changed
-        (data pointer or in-place version counter)."""
+        """Device blob for this stack, rebuilt only when a parameter or a
+        permutation changed (storage or in-place version counter)."""
         ps = self.param_tensors()
         for p in ps:
             if p.device != device or p.dtype != torch.float32:
                 raise TypeError("native coupling path needs fp32 parameters on %s" % device)
-        key = tuple((p.data_ptr(), p._version) for p in ps)
+        if self._perm_state() != self._perm_key:
+            self._refresh_desc()
+            self._cache.clear()
+        key = self.state_key()
         ent = self._cache.get(device)
         if ent is not None and ent[0] == key:
             return ent[1]
@@ -114,12 +157,13 @@ class CouplingStack:
             raise ValueError("expected [B, %d] logits, got %s" % (self.dim, tuple(x.shape)))
         return x.contiguous()
 
-    def run(self, x, inverse=False, want_all=False, want_final=True):
+    def run(self, x, inverse=False, want_all=False, want_final=True, blob=None):
         """Returns (final [B,D] or None, logdet [B], all [L,B,D] or None)."""
         x = self._check_input(x)
         B = x.shape[0]
         dev = x.device
-        blob = self.prepared(dev)
+        if blob is None:
+            blob = self.prepared(dev)
         ld = torch.empty(B, dtype=torch.float32, device=dev)
         allt = torch.empty(self.L, B, self.dim, dtype=torch.float32, device=dev) \
             if want_all else None
@@ -137,7 +181,8 @@ class CouplingStack:
 
     def forward_loss(self, x, y, kind=_lib.LOSS_CAL, det=1.0, want_outputs=False):
         """Fused forward + log-det + loss terms (cnf_forward_loss): returns
-        (terms[3] = sums over the rows of (loss, ce, log-det), z or None, ld or None)."""
+        (terms[3] = sums over the rows of (loss, ce, log-det), z or None, ld or None).
+        A label outside [0, D) makes the terms NaN (the reference raises)."""
         x = self._check_input(x)
         y = y.contiguous().to(torch.int64)
         B = x.shape[0]
@@ -148,10 +193,13 @@ class CouplingStack:
         _lib.check("cnf_forward_loss_workspace_bytes",
                    lib.cnf_forward_loss_workspace_bytes(ctypes.byref(self.desc),
                                                         ctypes.c_int64(B), ctypes.byref(n)))
-        ws = self._loss_ws.get(dev)
+        # one workspace per (device, stream): launches on two streams never share
+        # the partial-sum records
+        sk = _stream_key(dev)
+        ws = self._loss_ws.get(sk)
         if ws is None or ws.numel() < n.value:
-            ws = torch.zeros(max(n.value, 16), dtype=torch.uint8, device=dev)  # ticket = 0
-            self._loss_ws[dev] = ws
+            ws = torch.zeros(max(n.value, 16), dtype=torch.uint8, device=dev)
+            self._loss_ws[sk] = ws
         terms = torch.empty(3, dtype=torch.float32, device=dev)
         z = torch.empty_like(x) if want_outputs else None
         ld = torch.empty(B, dtype=torch.float32, device=dev) if want_outputs else None
@@ -163,6 +211,33 @@ class CouplingStack:
         stats["forward"] += 1
         return terms, z, ld
 
+    def predict(self, x, log_priors, want_logdet=False):
+        """Calibrated probabilities softmax(log(softmax(flow(x - mean x)) + 1e-7)
+        - log_priors) (Calibrator.predict, calibrators.py:40-44, 330-353):
+        one fused cnf_predict launch, or -- for shapes it does not cover --
+        cnf_forward followed by the same math as device torch ops."""
+        x = self._check_input(x)
+        B = x.shape[0]
+        dev = x.device
+        lp = torch.as_tensor(log_priors, dtype=torch.float32, device=dev).reshape(-1).contiguous()
+        if lp.numel() != self.dim:
+            raise ValueError("log_priors must have %d entries" % self.dim)
+        blob = self.prepared(dev)
+        probs = torch.empty_like(x)
+        ld = torch.empty(B, dtype=torch.float32, device=dev) if want_logdet else None
+        st = _lib.lib().cnf_predict(ctypes.byref(self.desc), _ptr(blob), _ptr(x), _ptr(lp),
+                                    _ptr(probs), _ptr(ld), ctypes.c_int64(B), _stream(dev))
+        if st == 0:
+            stats["predict"] += 1
+            return (probs, ld) if want_logdet else probs
+        if st != -3:
+            _lib.check("cnf_predict", st)
+        xc = x - x.mean(dim=1, keepdim=True)
+        z, ld, _ = self.run(xc, blob=blob)
+        p = torch.softmax(z, dim=1)
+        probs = torch.softmax(torch.log(p + 1e-7) - lp, dim=1)
+        return (probs, ld) if want_logdet else probs
+
     # -------------------------------------------------------------- autograd
     def forward_autograd(self, x, want_all):
         """Forward with gradients w.r.t. x and every parameter (cnf_vjp)."""
@@ -173,9 +248,12 @@ class CouplingStack:
 class _StackFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, stack, want_all, x, *params):
-        fin, ld, allt = stack.run(x, inverse=False, want_all=want_all)
+        blob = stack.prepared(x.device)
+        fin, ld, allt = stack.run(x, inverse=False, want_all=want_all, blob=blob)
         ctx.stack = stack
         ctx.want_all = want_all
+        ctx.blob = blob
+        ctx.key = stack.state_key()
         ctx.save_for_backward(x)
         return (allt if want_all else fin), ld
 
@@ -184,8 +262,13 @@ class _StackFn(torch.autograd.Function):
         from .vjp import stack_vjp
         (x,) = ctx.saved_tensors
         stack = ctx.stack
+        if stack.state_key() != ctx.key:
+            raise RuntimeError(
+                "one of the variables needed for gradient computation has been modified by an "
+                "inplace operation: a coupling-layer weight or permutation changed between the "
+                "native forward and its backward")
         dx, grads = stack_vjp(stack, x, g_out, g_ld, all_grads=ctx.want_all,
-                              need_dx=ctx.needs_input_grad[2])
+                              need_dx=ctx.needs_input_grad[2], blob=ctx.blob)
         ps = stack.param_tensors()
         out = [None, None, dx]
         for p, g in zip(ps, grads):

@@ -11,18 +11,20 @@ import warnings
 import torch
 
 from . import _lib
-from .engine import _ptr, _stream, stats
+from .engine import _ptr, _stream, _stream_key, stats
 
 _ws_cache = {}
 
 
 def _workspace(stack, B, device):
+    """Per-block gradient partials: one buffer per (device, stream), so launches
+    on different streams never share it; grown on demand."""
     lib = _lib.lib()
     n = ctypes.c_size_t()
     _lib.check("cnf_vjp_workspace_bytes",
                lib.cnf_vjp_workspace_bytes(ctypes.byref(stack.desc), ctypes.c_int64(B),
                                            ctypes.byref(n)))
-    key = (device, stack.desc.dim)
+    key = _stream_key(device)
     buf = _ws_cache.get(key)
     if buf is None or buf.numel() < n.value:
         buf = torch.empty(max(n.value, 16), dtype=torch.uint8, device=device)
@@ -39,14 +41,16 @@ def _split(stack, flat):
     return out
 
 
-def stack_vjp(stack, x, g_out, g_ld, all_grads, need_dx):
+def stack_vjp(stack, x, g_out, g_ld, all_grads, need_dx, blob=None):
     """(dx or None, [grad per parameter]) for the upstream gradients of
-    (z_all if all_grads else z_final, log-det)."""
+    (z_all if all_grads else z_final, log-det); `blob`: the prepared weights
+    the forward ran with."""
     x = x.contiguous()
     B = x.shape[0]
     dev = x.device
     try:
-        blob = stack.prepared(dev)
+        if blob is None:
+            blob = stack.prepared(dev)
         ws, nws = _workspace(stack, B, dev)
     except _lib.UnsupportedShape:
         return _torch_vjp(stack, x, g_out, g_ld, all_grads, need_dx)
@@ -104,6 +108,9 @@ def _torch_vjp(stack, x, g_out, g_ld, all_grads, need_dx):
     """Shapes without a native VJP (strict-NaN mode, the MFMA-tile family):
     autograd through the layers' own torch ops, on the same device."""
     key = (stack.dim, tuple(stack.hidden), stack.strict_nan)
+    from flows.flows import STRICT_NATIVE
+    if STRICT_NATIVE:
+        raise RuntimeError("native coupling path unavailable: no native VJP for %s" % (key,))
     if key not in _warned:
         _warned.add(key)
         warnings.warn("cnf: no native VJP for %s; using torch autograd" % (key,), RuntimeWarning)

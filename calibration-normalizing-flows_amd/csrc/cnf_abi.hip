@@ -27,6 +27,8 @@ int derive_shape(const cnf_desc* d, Shape* s) {
   s->scale = d->scale;
   s->shift = d->shift;
   s->strict = d->strict_nan ? 1 : 0;
+  if (d->options & ~(CNF_OPT_NO_SGPR | CNF_OPT_NO_WIDE)) return CNF_ERR_DESC;
+  s->options = d->options;
   s->nets = d->scale + d->shift;
   s->n_lin = d->n_hidden + 1;       // units = [dim] + hidden + [dim]  (flows/utils.py:14)
   s->units[0] = d->dim;
@@ -221,6 +223,21 @@ int cnf_forward_loss(const cnf_desc* desc, const void* prepared, const float* x,
     return CNF_ERR_HIP;
   }
   return CNF_OK;
+}
+
+int cnf_predict(const cnf_desc* desc, const void* prepared, const float* x,
+                const float* log_priors, float* probs, float* logdet, int64_t B, void* stream) {
+  Shape s;
+  int st = derive_shape(desc, &s);
+  if (st != CNF_OK) return st;
+  if (B < 0) return CNF_ERR_BATCH;
+  if (s.family != Family::kValu || !sgpr_enabled(s)) return CNF_ERR_UNSUPPORTED;
+  if (B == 0) return CNF_OK;
+  if (!prepared || !x || !log_priors || !probs) return CNF_ERR_NULL;
+  auto mis = [](const void* p) { return p && (reinterpret_cast<uintptr_t>(p) & 3); };
+  if (mis(x) || mis(probs) || mis(logdet) || mis(log_priors)) return CNF_ERR_ALIGN;
+  return sgpr_run(s, prepared, x, probs, logdet, nullptr, B, false, (hipStream_t)stream, nullptr,
+                  nullptr, 0, 0.f, nullptr, log_priors);
 }
 
 int cnf_vjp_workspace_bytes(const cnf_desc* desc, int64_t B, size_t* bytes) {

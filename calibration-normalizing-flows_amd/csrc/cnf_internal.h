@@ -24,6 +24,7 @@ struct Shape {
   int n_lin = 0;                     // Linear layers per net
   int units[kMaxLin + 1] = {};       // [D, h..., D]
   int scale = 1, shift = 1, strict = 0;
+  int options = 0;                   // cnf_desc.options (CNF_OPT_*)
   int nets = 2;                      // scale + shift
   int64_t net_floats = 0;            // natural layout (state_dict order)
   int64_t layer_floats = 0;
@@ -75,9 +76,12 @@ int valu_run(const Shape& s, const void* prepared, const float* in, float* out, 
 int valu_loss_blocks(const Shape& s, int64_t B);  // per-block loss partials of the fused eval
 bool sgpr_enabled(const Shape& s);
 int64_t sgpr_blocks(const Shape& s, int64_t B);
+// CNF_ERR_UNSUPPORTED when this launch needs k_valu (permuted loss/predict,
+// misaligned batch views); log_priors != NULL: the fused predict pass
 int sgpr_run(const Shape& s, const void* prepared, const float* in, float* out, float* ld,
              float* all, int64_t B, bool inverse, hipStream_t st, const int64_t* y,
-             float* loss_ws, int kind, float det, float* loss_terms);
+             float* loss_ws, int kind, float det, float* loss_terms,
+             const float* log_priors = nullptr);
 // sum partials[b][i] over b in block order: grads[i] (i < P), terms[i - P] (i < P + 3)
 int reduce_partials(const float* partials, int nblk, int PS, int P, float* grads, float* terms,
                     hipStream_t st);

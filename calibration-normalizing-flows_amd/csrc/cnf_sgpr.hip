@@ -1,37 +1,71 @@
-// Fused multi-layer coupling kernel, pipelined-scalar-weight form, for the
-// narrow calibration flows whose every conditioner Linear fits 32 floats
-// (W[nout][nin] + b[nout]: the reference default D=10, hidden_size=[5,5],
-// flows/flows.py:71, is three 5x5 Linears per net).
+// Fused multi-layer coupling kernel for the narrow calibration flows whose
+// every conditioner Linear fits 32 floats (W[nout][nin] + b[nout]: the
+// reference default D=10, hidden_size=[5,5], flows/flows.py:71, is three 5x5
+// Linears per net).  Serves every final-output launch of those shapes:
+// forward (+log-det), inverse, the fused calibrator eval loss, the fused
+// predict pass, and every-layer outputs (the reference's zs / xs lists).
 //
-// Same math and tile/row layout as k_valu (cnf_valu.hip header comment,
-// flows/flows.py:101-126), different weight path: every Linear's block is
-// pulled into SGPRs by two s_load_dwordx16 issued one Linear AHEAD of its use
-// (double-buffered, 64 SGPRs), so
-//   * each FMA takes its weight as an SGPR operand (op_sel picks the half),
-//     with no VGPR copies of weights and no LDS broadcast traffic;
-//   * the scalar-cache round trip of a Linear overlaps the previous Linear's
-//     FMAs instead of stalling the wave once per output neuron.
-// The s-net's last Linear is stored pre-multiplied by log2(e) (cnf_prepare), so
-// exp(s) is one v_exp_f32 and the log-det is ln2 * sum(s') once per row.
-// Non-strict only (strict_nan keeps k_valu); shift must be on (NICE: s = 0).
+// Reference semantics restated (paths in the reference repo):
+//   MLP.forward                 flows/utils.py:26-31
+//   NvpCouplingLayer.forward    flows/flows.py:101-112
+//       z = m*x + (1-m)*(x*exp(s) + t);  ld = sum((1-m)*s);  z = z[:,perm]; z.flip(1)
+//   NvpCouplingLayer.backward   flows/flows.py:114-126  (the INVERSE)
+//       z = z.flip(1); z = z[:,rev_perm]; x = m*z + (1-m)*(z-t)*exp(-s); ld = -sum((1-m)s)
+//   Flow.forward / backward     flows/flows.py:17-37
+//   calibrator loss terms       calibrators.py:287-291, 297-317 (CE variant:
+//                               run_experiment3D.py:107)
+//   predict                     calibrators.py:40-44, 330-353:
+//       softmax(log(softmax(flow(x - mean x)) + 1e-7) - log_priors)
+//
+// Work layout.  A WAVE owns a tile of 128 consecutive rows; lane l holds rows
+// 2l and 2l+1 as one packed pair per feature, so every conditioner FMA is one
+// v_pk_fma_f32 for two rows with the weight as an SGPR operand:
+//   * weights: each Linear's block is pulled into SGPRs by s_load_dwordx16
+//     issued one Linear ahead of its use (double-buffered, 64 SGPRs); the
+//     bias rides the first FMA of each neuron as the high half of its weight's
+//     SGPR pair (op_sel);
+//   * ReLU costs nothing: the hidden Linears are stored scaled by 2^-64
+//     (cnf_prepare) so relu(a) * 2^-64 = clamp(a * 2^-64, 0, 1) is the clamp
+//     bit of the neuron's last FMA; the next Linear's input columns carry the
+//     2^64 back (powers of two: exact, no rounding change).  Activations past
+//     2^64 (1.8e19) would saturate -- those rows overflow exp(s) anyway;
+//   * the s-net's last Linear is stored pre-multiplied by log2(e), so exp(s) is
+//     one v_exp_f32 and the log-det is ln2 * sum(s');
+//   * input: the wave's next tile streams HBM -> LDS by LDS-DMA
+//     (global_load_lds_dwordx4, no VGPRs) while the current tile computes; a
+//     lane's two rows are 2*D contiguous floats, so each feature pair is one
+//     ds_read2_b32 straight into a packed register pair;
+//   * output: the lane's 2*D contiguous output floats leave as 16-B stores from
+//     registers, issued one tile LATE (after the next tile's LDS reads), so the
+//     wave's wait for its DMA never waits on stores it has just issued;
+//   * a persistent grid (CUs x resident blocks) walks the tiles wave by wave;
+//     s_setprio by tiles remaining (longest-remaining-first) keeps the SIMDs'
+//     oldest-first arbitration from leaving a long single-wave tail.
+// Every variant is compile-time (mode, random_flip, every-layer stores), so
+// the hot loop has no data-dependent branches and no scratch.
 #include <hip/hip_runtime.h>
 
-#include <cstdlib>
 #include <mutex>
+#include <type_traits>
 #include <unordered_map>
 
 #include "cnf_internal.h"
 #include "cnf_valu_common.h"
 #include "cnf_valu_io.h"
 
-#ifndef CNF_SGPR_WPE
-#define CNF_SGPR_WPE 5
-#endif
-
-#ifdef CNF_TIMELINE
-// Diagnostic build only (make timeline): per-block wall-clock marks of the
-// persistent kernel, s_memrealtime (100 MHz): [start, first tile ready, end, hw id]
-__device__ unsigned long long cnf_tl[4096 * 4];
+#ifdef CNF_SGPR_TRACE
+// Diagnostic build only (make trace, never shipped): per-wave s_memrealtime
+// (100 MHz) marks [start, tile0 data, tile0 done, tile1 data, tile1 done,
+// last tile done, end, hw id] of the last launch, read by tools/sgpr_trace.py.
+__device__ unsigned long long cnf_trace[16384 * 8];
+#define CNF_TR(slot)                                                                   \
+  do {                                                                                 \
+    if (lane == 0 && gw < 16384) cnf_trace[gw * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define CNF_TR(slot) \
+  do {               \
+  } while (0)
 #endif
 
 namespace cnf {
@@ -39,23 +73,14 @@ namespace {
 
 using namespace valu;
 
-#ifdef CNF_TIMELINE
-__device__ __forceinline__ void tl_mark(int slot) {
-  if (threadIdx.x == 0 && blockIdx.x < 4096) {
-    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
-    cnf_tl[blockIdx.x * 4 + slot] = t;
-    if (slot == 0)
-      cnf_tl[blockIdx.x * 4 + 3] =
-          ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
-          __builtin_amdgcn_s_getreg((31 << 11) | 4);  // XCC_ID, HW_ID
-  }
-}
-#define CNF_TL(slot) tl_mark(slot)
-#else
-#define CNF_TL(slot)
-#endif
+constexpr int kWaves = 4;   // waves per block
+constexpr int kTR = 128;    // rows per wave tile (lane l: rows 2l, 2l+1)
+constexpr int kWPE = 5;        // register budget: resident waves per SIMD
 
-// Compile-time SP layout of one net (must match derive_shape's sp_lin_off).
+enum Mode { kFwd = 0, kInv = 1, kLoss = 2, kPredict = 3 };
+
+// Compile-time layout of one net in the packed-SGPR region (must match
+// derive_shape's sp_lin_off and cnf_prepare's mode 3).
 template <int D, int H1, int H2>
 struct SP {
   static constexpr int DT = D / 2, DC = D - D / 2;
@@ -83,24 +108,31 @@ struct SW {
 };
 
 // w0 * x + b with (w0, b) ONE SGPR pair: op_sel broadcasts the low half as the
-// multiplier and the high half as the addend, so the bias costs no VALU move
-// (a pair read twice is one constant-bus operand).
+// multiplier and the high half as the addend, so the bias costs no VALU move.
 __device__ __forceinline__ f2 fma_wb(f2 wb, f2 x) {
   f2 a;
   asm("v_pk_fma_f32 %0, %1, %2, %1 op_sel:[0,0,1] op_sel_hi:[0,1,1]" : "=v"(a) : "s"(wb), "v"(x));
   return a;
 }
+// ... and the clamped forms that end a hidden neuron (relu folded, see header)
+__device__ __forceinline__ f2 fma_wb_clamp(f2 wb, f2 x) {
+  f2 a;
+  asm("v_pk_fma_f32 %0, %1, %2, %1 op_sel:[0,0,1] op_sel_hi:[0,1,1] clamp"
+      : "=v"(a) : "s"(wb), "v"(x));
+  return a;
+}
+__device__ __forceinline__ f2 fma_clamp(float w, f2 x, f2 acc) {
+  f2 a;
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1] clamp" : "=v"(a) : "s"(f2{w, w}), "v"(x),
+      "v"(acc));
+  return a;
+}
 
 // Issue the loads of one Linear block: plain (compiler-visible) scalar loads,
-// so the compiler's own s_waitcnt insertion guards every read of the
-// destination SGPRs -- including any copy or spill the register allocator
-// adds -- and a sched_barrier keeps the load from sinking toward its use:
-// ALU work may cross it, memory operations may not, so the block's
-// s_load_dwordx16 pair issues one Linear ahead of its first FMA.
-// (An earlier form issued the s_load from inline asm and waited in a second
-// asm statement; the allocator was then free to copy the in-flight
-// destination registers between the two -- seen as s_mov_b64 of a pending
-// s_load_dwordx16 destination -- i.e. to read weights before they landed.)
+// so the compiler's own s_waitcnt guards every read of the destination SGPRs
+// (copies and spills included); the sched_barriers keep the block's
+// s_load_dwordx16s one Linear ahead of their first use.  (An inline-asm
+// load/wait pair let the register allocator copy still-in-flight SGPRs.)
 template <int NC>
 __device__ __forceinline__ void sissue(SW<NC>& r, const float* p) {
   const v16f* q = reinterpret_cast<const v16f*>(__builtin_assume_aligned(p, 64));
@@ -109,27 +141,27 @@ __device__ __forceinline__ void sissue(SW<NC>& r, const float* p) {
   for (int i = 0; i < NC; ++i) r.c[i] = q[i];
   __builtin_amdgcn_sched_barrier(0);
 }
-// End of the Linear that overlaps the load: nothing crosses, so the next
-// Linear's FMAs (the loaded block's consumers) cannot be hoisted up to the load.
 template <int NC>
 __device__ __forceinline__ void swait(SW<NC>&) {
   __builtin_amdgcn_sched_barrier(0);
 }
 
 // y[o] = b[o] + sum_k W[o][k] x[k] from an SGPR block of rows
-// [w_o0, b_o, w_o1 .. w_o(NIN-1)] at stride S (even)
-// after(): issued once the first output neuron is done (the next block's load:
-// the compiler's wait for THIS block then precedes it, so an SMEM lgkmcnt(0)
-// never has to cover the load just issued).
-template <int NIN, int NOUT, int S, bool RELU, int NC, class T, class F>
-__device__ __forceinline__ void slin(const SW<NC>& w, const T* x, T* y, F&& after) {
-  static_assert(sizeof(T) == 8, "pipelined-scalar kernel packs two rows per lane");
+// [w_o0, b_o, w_o1 .. w_o(NIN-1)] at stride S; RELU: clamped last FMA.
+// after(): issued once the first output neuron is done (the next block's load).
+template <int NIN, int NOUT, int S, bool RELU, int NC, class F>
+__device__ __forceinline__ void slin(const SW<NC>& w, const f2* x, f2* y, F&& after) {
 #pragma unroll
   for (int o = 0; o < NOUT; ++o) {
-    T a = fma_wb(w.pair(o * S), x[0]);
+    f2 a;
+    if constexpr (RELU && NIN == 1) a = fma_wb_clamp(w.pair(o * S), x[0]);
+    else a = fma_wb(w.pair(o * S), x[0]);
 #pragma unroll
-    for (int k = 1; k < NIN; ++k) a = fmaT(w[o * S + 1 + k], x[k], a);
-    y[o] = RELU ? relu<false>(a) : a;
+    for (int k = 1; k < NIN; ++k) {
+      if (RELU && k == NIN - 1) a = fma_clamp(w[o * S + 1 + k], x[k], a);
+      else a = fmaT(w[o * S + 1 + k], x[k], a);
+    }
+    y[o] = a;
     if (o == 0) after();
   }
 }
@@ -137,12 +169,10 @@ __device__ __forceinline__ void slin(const SW<NC>& w, const T* x, T* y, F&& afte
 // Linear IDX of the layer's sequence (net-major: s-net Linears, then t-net);
 // the next block (or the next layer's first, wn) is issued before computing.
 // The two SGPR buffers alternate by the Linear's parity in the layer pair
-// (PAR: parity of the layer's first Linear) -- never a `cur = nxt` copy: a
-// copy gives the compiler a reason to move the in-flight destination of an
-// s_load into other registers before the s_waitcnt (seen: s_mov_b64 of a
-// pending s_load_dwordx16 destination), i.e. to read it before it lands.
-template <class S, int NETS, int IDX, int PAR, class T>
-__device__ __forceinline__ void run_seq(const T* c, T* h1, T* h2, T* s, T* t, SW<S::NC>& A,
+// (PAR) -- never a `cur = nxt` copy, which would let the compiler move an
+// in-flight s_load destination before its wait.
+template <class S, int NETS, int IDX, int PAR, bool NEXT>
+__device__ __forceinline__ void run_seq(const f2* c, f2* h1, f2* h2, f2* s, f2* t, SW<S::NC>& A,
                                         SW<S::NC>& Bf, const float* wl, const float* wn) {
   if constexpr (IDX < NETS * S::NL) {
     constexpr int net = IDX / S::NL, i = IDX % S::NL;
@@ -150,45 +180,48 @@ __device__ __forceinline__ void run_seq(const T* c, T* h1, T* h2, T* s, T* t, SW
     SW<S::NC>& cur = odd ? Bf : A;
     SW<S::NC>& nxt = odd ? A : Bf;
     constexpr bool last = i == S::NL - 1;
-    const T* in = i == 0 ? c : (i == 1 ? h1 : h2);
-    T* out = last ? ((NETS == 2 && net == 0) ? s : t) : (i == 0 ? h1 : h2);
+    const f2* in = i == 0 ? c : (i == 1 ? h1 : h2);
+    f2* out = last ? ((NETS == 2 && net == 0) ? s : t) : (i == 0 ? h1 : h2);
     slin<S::nin(i), S::nout(i), S::stride(i), !last>(cur, in, out, [&]() {
       if constexpr (IDX + 1 < NETS * S::NL)
         sissue(nxt, wl + ((IDX + 1) / S::NL) * S::NF + S::off((IDX + 1) % S::NL));
-      else
+      else if constexpr (NEXT)
         sissue(nxt, wn);
     });
     swait(nxt);
-    run_seq<S, NETS, IDX + 1, PAR>(c, h1, h2, s, t, A, Bf, wl, wn);
+    run_seq<S, NETS, IDX + 1, PAR, NEXT>(c, h1, h2, s, t, A, Bf, wl, wn);
   }
 }
 
-// One coupling layer, input in orientation O, output in orientation !O
-// (k_valu's step(), non-strict, weights from the pipelined SGPR buffer).
-// O is also the layer's position in its pair (the odd tail layer is a first):
-// the second layer's Linears start on buffer parity NETS * NL.
-template <int D, int H1, int H2, bool INV, bool O, int NETS, class T>
-__device__ __forceinline__ void sp_step(T* v, T& ld, SW<SP<D, H1, H2>::NC>& A,
+// One coupling layer, input in orientation O (O: row held reversed), output in
+// orientation !O -- the flip is a register renaming.  O is also the layer's
+// position in its pair (the second layer's Linears start on buffer parity
+// NETS * NL).  NEXT: prefetch the next layer's first block (wn) -- the pair's
+// first layer does; the pair's last does not, so no SGPR buffer lives across
+// the layer loop's back-edge (a loop-carried buffer makes the allocator rotate
+// it through spill lanes).
+template <int D, int H1, int H2, bool INV, bool O, int NETS, bool PERM, bool NEXT>
+__device__ __forceinline__ void sp_step(f2* v, f2& ld, SW<SP<D, H1, H2>::NC>& A,
                                         SW<SP<D, H1, H2>::NC>& Bf, const float* wl,
                                         const float* wn, bool perm,
                                         const int32_t* __restrict__ q) {
   using S = SP<D, H1, H2>;
   constexpr int DT = S::DT, DC = S::DC;
   constexpr bool OC = INV ? !O : O;
-  if constexpr (INV) {
+  if constexpr (INV && PERM) {
     if (perm) permute<D, O>(v, q);  // flows/flows.py:115-117
   }
-  T c[DC];
+  f2 c[DC];
 #pragma unroll
   for (int k = 0; k < DC; ++k) c[k] = v[R<D, OC>(DT + k)];
-  T h1[H1 > 0 ? H1 : 1], h2[H2 > 0 ? H2 : 1], s[DT], t[DT];
-  run_seq<S, NETS, 0, O ? (NETS * S::NL) & 1 : 0>(c, h1, h2, s, t, A, Bf, wl, wn);
+  f2 h1[H1 > 0 ? H1 : 1], h2[H2 > 0 ? H2 : 1], s[DT], t[DT];
+  run_seq<S, NETS, 0, O ? (NETS * S::NL) & 1 : 0, NEXT>(c, h1, h2, s, t, A, Bf, wl, wn);
 #pragma unroll
   for (int j = 0; j < DT; ++j) {
-    T& x = v[R<D, OC>(j)];
+    f2& x = v[R<D, OC>(j)];
     if constexpr (NETS == 1) {  // scale=False: s = 0, exp(0) = 1, log-det += 0
       x = INV ? x - t[j] : x + t[j];
-    } else if constexpr (!INV) {  // s[j] = log2(e) * s (scaled at prepare): exp(s) = 2^s[j]
+    } else if constexpr (!INV) {  // s[j] = log2(e) * s: exp(s) = 2^s[j]
       x = fmaV(x, exp2T(s[j]), t[j]);
       ld += s[j];
     } else {
@@ -196,195 +229,404 @@ __device__ __forceinline__ void sp_step(T* v, T& ld, SW<SP<D, H1, H2>::NC>& A,
       ld -= s[j];
     }
   }
-  if constexpr (!INV) {
+  if constexpr (!INV && PERM) {
     if (perm) permute<D, O>(v, q);  // flows/flows.py:110-112
   }
 }
 
-// Async copy of one full input tile (TF floats, 16-B aligned) into LDS: every
-// wave moves 1 KiB per global_load_lds_dwordx4, lane-linear (the tile is
-// contiguous in HBM and in LDS, so the image is the row-major tile itself).
-template <int ROWS, int TF>
-__device__ __forceinline__ void tile_prefetch(float* sm, const float* __restrict__ src) {
-  static_assert(TF % 4 == 0, "tile must be whole float4s");
-  constexpr int N4 = TF / 4, NI = (N4 + 63) / 64, NW = ROWS / 64;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+// ---------------------------------------------------------------------------
+// tile I/O: a lane's two rows are the 2*D contiguous floats at row 2l
+// ---------------------------------------------------------------------------
+// HBM -> LDS copy of one full wave tile (128*D floats, 16-B aligned) by
+// LDS-DMA: one global_load_lds_dwordx4 moves 1 KiB, lane-linear.
+template <int D>
+__device__ __forceinline__ void wave_dma(float* sm, const float* __restrict__ src, int lane) {
+  constexpr int N4 = 32 * D, NI = (N4 + 63) / 64;
 #pragma unroll
-  for (int i = 0; i < (NI + NW - 1) / NW; ++i) {
-    const int c = (i * NW + w) * 64;  // first float4 of this wave's 1 KiB
-    if (c + lane < N4)
-      __builtin_amdgcn_global_load_lds(src + (int64_t)(c + lane) * 4,
-                                       (__attribute__((address_space(3))) void*)(sm + c * 4), 16,
+  for (int i = 0; i < NI; ++i) {
+    if (N4 % 64 == 0 || i * 64 + lane < N4)
+      __builtin_amdgcn_global_load_lds(src + (i * 64 + lane) * 4,
+                                       (__attribute__((address_space(3))) void*)(sm + i * 256), 16,
                                        0, 0);
   }
 }
 
-// Per-wave form: wave w copies only the rows it owns (rows q*ROWS + 64w ..
-// +63 of the tile, RW contiguous 64*D-float chunks) into the same place of the
-// LDS image, so it waits on its own vmcnt and needs no block barrier before
-// reading them or before refilling them with the next tile.
-template <int D, int ROWS, int RW>
-__device__ __forceinline__ void wave_prefetch(float* sm, const float* __restrict__ src) {
-  constexpr int N4 = 16 * D;  // float4s per 64-row chunk
-  const int lane = threadIdx.x & 63;
-  // wave-uniform chunk bases in SGPRs; one lane-offset VGPR for every copy
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+// rows 2l, 2l+1 of the LDS tile as packed pairs (one ds_read2_b32 each)
+template <int D>
+__device__ __forceinline__ void read_pairs(const float* sm, int lane, f2* v) {
+  const float* p = sm + 2 * D * lane;
 #pragma unroll
-  for (int q = 0; q < RW; ++q) {
-    const int c0 = (q * ROWS + 64 * w) * D / 4;  // first float4 of the chunk
-    const float* base = src + (int64_t)c0 * 4;
+  for (int k = 0; k < D; ++k) v[k] = f2{p[k], p[D + k]};
+}
+
+// A lane's 2*D output floats (pairs in logical order) to dst = row 2l:
+// 16-B stores when aligned, else 8-B, else 4-B; `rows` < 2 on the ragged tile.
+template <int D>
+__device__ __forceinline__ void store_pairs(float* __restrict__ dst, const f2* v, int rows,
+                                            int al) {
+  constexpr int NF = 2 * D;
+  float r[NF];
 #pragma unroll
-    for (int i = 0; i < (N4 + 63) / 64; ++i) {
-      if (i * 64 + lane < N4)
-        __builtin_amdgcn_global_load_lds(base + (i * 64 + lane) * 4,
-                                         (__attribute__((address_space(3))) void*)(sm + (c0 + i * 64) * 4),
-                                         16, 0, 0);
-    }
+  for (int k = 0; k < D; ++k) {
+    r[k] = v[k].x;
+    r[D + k] = v[k].y;
+  }
+  if (rows == 2 && NF % 4 == 0 && al >= 16) {
+#pragma unroll
+    for (int q = 0; q < NF / 4; ++q)
+      reinterpret_cast<float4*>(dst)[q] = float4{r[4 * q], r[4 * q + 1], r[4 * q + 2], r[4 * q + 3]};
+  } else if (rows == 2 && NF % 2 == 0 && al >= 8) {
+#pragma unroll
+    for (int q = 0; q < NF / 2; ++q) reinterpret_cast<float2*>(dst)[q] = float2{r[2 * q], r[2 * q + 1]};
+  } else {
+#pragma unroll
+    for (int k = 0; k < NF; ++k)
+      if (k < rows * D) dst[k] = r[k];
   }
 }
 
-// PIPE: persistent grid (CUs x resident blocks) walking the tiles; while a
-// tile computes, the next full tile streams into the LDS tile by LDS-DMA (no
-// VGPRs), and outputs go straight from registers to HBM.
-// PIPE: 0 one tile per block, 1 persistent + block-wide DMA, 2 persistent +
-// per-wave DMA (no barriers on the tile path).
-template <int D, int H1, int H2, bool INV, int NETS, int RW, int ROWS, int PIPE>
-__global__ __launch_bounds__(ROWS, INV ? CNF_SGPR_WPE - 1 : CNF_SGPR_WPE) void k_sgpr(
-    const float* __restrict__ W, const int32_t* __restrict__ qtab,
-    const int32_t* __restrict__ lflag, const float* __restrict__ in, float* __restrict__ out,
-    float* __restrict__ ld_out, float*, int64_t B, int L, int prio_mode, int,
-    int any_perm, int vec_io, const int64_t* __restrict__ yl, float* __restrict__ loss_part,
-    int kind, float det, unsigned* __restrict__ ticket, float* __restrict__ loss_terms) {
+__device__ __forceinline__ void store_ld2(float* __restrict__ dst, f2 ld, int rows, bool al8) {
+  if (rows == 2 && al8) {
+    *reinterpret_cast<float2*>(dst) = float2{ld.x, ld.y};
+  } else {
+    if (rows > 0) dst[0] = ld.x;
+    if (rows > 1) dst[1] = ld.y;
+  }
+}
+
+// reverse the logical order of a row held in orientation 1 (odd L): afterwards
+// v[j] is logical j, so the epilogues have one form
+template <int D>
+__device__ __forceinline__ void unflip(f2* v) {
+#pragma unroll
+  for (int k = 0; k < D / 2; ++k) {
+    const f2 a = v[k];
+    v[k] = v[D - 1 - k];
+    v[D - 1 - k] = a;
+  }
+}
+
+// Labels of the lane's rows 2l, 2l+1 (int64 each, one 16-B load when aligned).
+// A label is valid iff 0 <= y < D; an invalid one poisons the loss terms with
+// NaN (the reference's probs.gather raises on it).  rows: valid rows (0..2).
+struct Lab {
+  int y0, y1;
+  bool ok0, ok1;
+};
+template <int D>
+__device__ __forceinline__ Lab load_labels2(const int64_t* __restrict__ y, int rows, bool al16) {
+  Lab r{0, 0, true, true};
+  int lo0 = 0, hi0 = 0, lo1 = 0, hi1 = 0;
+  const int32_t* y32 = reinterpret_cast<const int32_t*>(y);
+  if (rows == 2 && al16) {
+    const int4 q = *reinterpret_cast<const int4*>(y32);
+    lo0 = q.x, hi0 = q.y, lo1 = q.z, hi1 = q.w;
+  } else {
+    if (rows > 0) lo0 = y32[0], hi0 = y32[1];
+    if (rows > 1) lo1 = y32[2], hi1 = y32[3];
+  }
+  r.ok0 = hi0 == 0 && (unsigned)lo0 < (unsigned)D;
+  r.ok1 = hi1 == 0 && (unsigned)lo1 < (unsigned)D;
+  r.y0 = r.ok0 ? lo0 : 0;
+  r.y1 = r.ok1 ? lo1 : 0;
+  return r;
+}
+
+// Loss terms of the lane's rows (pairs in logical order):
+// CAL: loss = -(log(softmax(z)[y] + 1e-7) + ld)    calibrators.py:288-291
+// CE:  loss = -log_softmax(z)[y] - det * ld         run_experiment3D.py:107
+template <int D>
+__device__ __forceinline__ void pair_loss(const f2* v, f2 ld, const Lab& lab, int rows, int kind,
+                                          float det, float& t0, float& t1, float& t2) {
+  constexpr float kL2E = 1.4426950408889634f, kLN2 = 0.6931471805599453f;
+  f2 m = v[0];
+#pragma unroll
+  for (int j = 1; j < D; ++j) m = maxT(m, v[j]);
+  const f2 nm = m * splat(-kL2E, f2{});
+  f2 se = splat(0.f, f2{});
+#pragma unroll
+  for (int j = 0; j < D; ++j) se += exp2T(fmaT(kL2E, v[j], nm));
+  uint32_t za[D], zb[D];
+#pragma unroll
+  for (int j = 0; j < D; ++j) {
+    za[j] = __float_as_uint(v[j].x);
+    zb[j] = __float_as_uint(v[j].y);
+  }
+  const float zy[2] = {__uint_as_float(sel_tree<D>(za, lab.y0, 0)),
+                       __uint_as_float(sel_tree<D>(zb, lab.y1, 0))};
+  const bool ok[2] = {lab.ok0, lab.ok1};
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    if (q >= rows) continue;
+    const float lpy = zy[q] - (m[q] + __builtin_amdgcn_logf(se[q]) * kLN2);
+    const float l = ld[q];
+    float ce, loss;
+    if (kind == CNF_LOSS_CAL) {
+      ce = -__builtin_amdgcn_logf(__builtin_amdgcn_exp2f(lpy * kL2E) + 1e-7f) * kLN2;
+      loss = ce - l;
+    } else {
+      ce = -lpy;
+      loss = ce - det * l;
+    }
+    if (!ok[q]) ce = loss = __builtin_nanf("");
+    t0 += loss;
+    t1 += ce;
+    t2 += l;
+  }
+}
+
+// x - mean(x) per row (the calibrator centres logits before the flow,
+// calibrators.py:17,42)
+template <int D>
+__device__ __forceinline__ void centre(f2* v) {
+  f2 s = v[0];
+#pragma unroll
+  for (int j = 1; j < D; ++j) s += v[j];
+  const f2 mu = s * splat(1.f / D, f2{});
+#pragma unroll
+  for (int j = 0; j < D; ++j) v[j] -= mu;
+}
+
+// softmax(log(softmax(z) + 1e-7) - log_priors) per row, in place
+// (predict_post + Calibrator.predict, calibrators.py:40-44, 350-352)
+template <int D>
+__device__ __forceinline__ void pair_predict(f2* v, const float* __restrict__ lp) {
+  constexpr float kL2E = 1.4426950408889634f, kLN2 = 0.6931471805599453f;
+  f2 m = v[0];
+#pragma unroll
+  for (int j = 1; j < D; ++j) m = maxT(m, v[j]);
+  const f2 nm = m * splat(-kL2E, f2{});
+  f2 e[D], se = splat(0.f, f2{});
+#pragma unroll
+  for (int j = 0; j < D; ++j) {
+    e[j] = exp2T(fmaT(kL2E, v[j], nm));
+    se += e[j];
+  }
+  const f2 inv = f2{1.f / se.x, 1.f / se.y};
+  f2 a[D];
+#pragma unroll
+  for (int j = 0; j < D; ++j) {
+    const f2 p = e[j] * inv + splat(1e-7f, f2{});
+    a[j] = f2{__builtin_amdgcn_logf(p.x), __builtin_amdgcn_logf(p.y)} * splat(kLN2, f2{}) -
+           splat(lp[j], f2{});
+  }
+  f2 m2 = a[0];
+#pragma unroll
+  for (int j = 1; j < D; ++j) m2 = maxT(m2, a[j]);
+  const f2 nm2 = m2 * splat(-kL2E, f2{});
+  f2 s2 = splat(0.f, f2{});
+#pragma unroll
+  for (int j = 0; j < D; ++j) {
+    a[j] = exp2T(fmaT(kL2E, a[j], nm2));
+    s2 += a[j];
+  }
+  const f2 inv2 = f2{1.f / s2.x, 1.f / s2.y};
+#pragma unroll
+  for (int j = 0; j < D; ++j) v[j] = a[j] * inv2;
+}
+
+// Launch arguments besides the read-only tables, which travel as separate
+// __restrict__ kernel parameters: a pointer the compiler cannot prove
+// unaliased by the kernel's stores is read with vector loads, not s_load.
+struct KArgs {
+  const float* in;
+  float* out;             // final z / x / probabilities (nullable except predict)
+  float* ld;              // per-row log-det (nullable)
+  float* all;             // [L][B][D] every-layer outputs (ALL variants)
+  const int64_t* y;       // labels (loss)
+  float* part;            // per-block loss partials, 4 floats each (loss)
+  int64_t B;
+  int L, kind;
+  float det;
+};
+
+// The kernel.  MODE: kFwd / kInv (+ log-det), kLoss (forward + loss terms),
+// kPredict (centre + forward + calibrated probabilities).  ALL: also store
+// every layer's output.  PERM: some layer has a random_flip permutation.
+template <int D, int H1, int H2, int NETS, int MODE, bool ALL, bool PERM>
+__global__ __launch_bounds__(kWaves * 64, (MODE == kInv && PERM) ? kWPE - 1 : kWPE) void k_sgpr(
+    const float* __restrict__ W,        // packed-SGPR weight region
+    const int32_t* __restrict__ qtab,   // per-layer gather tables (forward or inverse)
+    const int32_t* __restrict__ lflag,  // per-layer flags
+    const float* __restrict__ lpri,     // log priors [D] (predict)
+    KArgs a) {
   using S = SP<D, H1, H2>;
-  using T = typename RowT<RW>::type;
-  constexpr int TR = ROWS * RW;
+  constexpr bool INV = MODE == kInv;
   constexpr int LF = NETS * S::NF;  // floats per layer
+  constexpr int TF = kTR * D;       // floats per wave tile
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* sm = smem;
-  const int tid = threadIdx.x;
-  const bool vec = vec_io != 0;
-  CNF_TL(0);
-  const int64_t ntiles = (B + TR - 1) / TR;
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  float* sm = smem + wv * TF;
+  const int64_t B = a.B;
+  const int L = a.L;
+  const int nfull = (int)(B / kTR), ntiles = (int)((B + kTR - 1) / kTR);
+  const int gw = blockIdx.x * kWaves + wv, nw = gridDim.x * kWaves;
+  int left = gw < ntiles ? (ntiles - 1 - gw) / nw + 1 : 0;  // tiles this wave owns
   auto layer_of = [&](int i) { return INV ? L - 1 - i : i; };
+  const int al_out = a.out ? (int)(reinterpret_cast<uintptr_t>(a.out) & 15) : 0;
+  const int al = al_out == 0 ? 16 : ((al_out & 7) == 0 ? 8 : 4);
+  const bool ld8 = a.ld && (reinterpret_cast<uintptr_t>(a.ld) & 7) == 0;
+  const bool y16 = MODE == kLoss && (reinterpret_cast<uintptr_t>(a.y) & 15) == 0;
+  float lp[MODE == kPredict ? D : 1];
+  if constexpr (MODE == kPredict) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) lp[j] = lpri[j];
+  }
   float lt0 = 0.f, lt1 = 0.f, lt2 = 0.f;
 
-  constexpr int TF = TR * D;
-  const int64_t nfull = B / TR;
-  const bool dma = PIPE && vec;
-  constexpr bool WDMA = PIPE == 2;
-  if (dma && (int64_t)blockIdx.x < nfull) {
-    if constexpr (WDMA) wave_prefetch<D, ROWS, RW>(sm, in + (int64_t)blockIdx.x * TF);
-    else tile_prefetch<ROWS, TF>(sm, in + (int64_t)blockIdx.x * TF);
-  }
-
-  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    if (prio_mode) {  // longest-remaining-first: blocks with more tiles left win issue
-      const int64_t rem = (ntiles - 1 - tile) / gridDim.x;  // tiles after this one
-      if (rem >= 3) __builtin_amdgcn_s_setprio(3);
-      else if (rem == 2) __builtin_amdgcn_s_setprio(2);
-      else if (rem == 1) __builtin_amdgcn_s_setprio(1);
-      else __builtin_amdgcn_s_setprio(0);
-    }
-    const int64_t row0 = tile * TR;
-    const int nrows = (int)((B - row0) < TR ? (B - row0) : TR);
-    SW<S::NC> cur, alt;
-    sissue(cur, W + (int64_t)layer_of(0) * LF);  // lands while the tile loads
-    int yv[RW];
-    if (loss_part) load_labels<RW>(yl, row0, tid, ROWS, B, yv);
-    if (dma && tile < nfull) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA has landed
-      if constexpr (!WDMA) lds_barrier();               // ... and every other wave's
-    } else {
-      lds_barrier();
-      tile_load<ROWS>(sm, in + row0 * D, nrows * D, vec);
-      lds_barrier();
-    }
-    T v[D];
+  // One tile's compute: rows in v (orientation 0) -> outputs in v (logical
+  // order), log-det in ld; every-layer stores on the way (rows valid: nr).
+  auto compute = [&](f2* v, f2& ld, int64_t row0, int nr) {
+    if constexpr (MODE == kPredict) centre<D>(v);
+    ld = splat(0.f, f2{});
+    auto st_all = [&](int i, auto O_) {
+      if constexpr (ALL) {
+        constexpr bool O = decltype(O_)::value;
+        f2 o[D];
 #pragma unroll
-    for (int k = 0; k < D; ++k) v[k] = get_row<ROWS>(sm, tid, D, k, T{});
-    if (tile == blockIdx.x) CNF_TL(1);
-    if (dma) {
-      const int64_t nt = tile + gridDim.x;
-      if (nt < nfull) {
-        if constexpr (WDMA) {
-          // this wave's rows are in registers once its LDS reads return
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          wave_prefetch<D, ROWS, RW>(sm, in + nt * TF);
-        } else {
-          lds_barrier();  // every wave has its rows in registers
-          tile_prefetch<ROWS, TF>(sm, in + nt * TF);
-        }
+        for (int j = 0; j < D; ++j) o[j] = v[R<D, O>(j)];
+        store_pairs<D>(a.all + ((int64_t)i * B + row0 + 2 * lane) * D, o, nr, al);
       }
-    }
-    swait(cur);
-    T ld = splat(0.f, T{});
+    };
     int i = 0;
     for (; i + 1 < L; i += 2) {
-      const int la = layer_of(i), lb = layer_of(i + 1), lc = layer_of(i + 2 < L ? i + 2 : 0);
-      const bool pa = any_perm && (lflag[la] & kFlagPerm);
-      const bool pb = any_perm && (lflag[lb] & kFlagPerm);
-      sp_step<D, H1, H2, INV, false, NETS>(v, ld, cur, alt, W + (int64_t)la * LF,
-                                           W + (int64_t)lb * LF, pa, qtab + la * D);
-      sp_step<D, H1, H2, INV, true, NETS>(v, ld, cur, alt, W + (int64_t)lb * LF,
-                                          W + (int64_t)lc * LF, pb, qtab + lb * D);
+      const int la = layer_of(i), lb = layer_of(i + 1);
+      const bool pa = PERM && (lflag[la] & kFlagPerm);
+      const bool pb = PERM && (lflag[lb] & kFlagPerm);
+      const float* wa = W + (int64_t)la * LF;
+      const float* wb = W + (int64_t)lb * LF;
+      SW<S::NC> cur, alt;
+      sissue(cur, wa);
+      swait(cur);
+      sp_step<D, H1, H2, INV, false, NETS, PERM, true>(v, ld, cur, alt, wa, wb, pa, qtab + la * D);
+      st_all(i, std::true_type{});
+      sp_step<D, H1, H2, INV, true, NETS, PERM, false>(v, ld, cur, alt, wb, nullptr, pb,
+                                                       qtab + lb * D);
+      st_all(i + 1, std::false_type{});
     }
-    const bool odd = i < L;
-    if (odd) {
+    if (i < L) {
       const int la = layer_of(i);
-      const bool pa = any_perm && (lflag[la] & kFlagPerm);
-      sp_step<D, H1, H2, INV, false, NETS>(v, ld, cur, alt, W + (int64_t)la * LF,
-                                           W + (int64_t)layer_of(0) * LF, pa, qtab + la * D);
+      const bool pa = PERM && (lflag[la] & kFlagPerm);
+      const float* wa = W + (int64_t)la * LF;
+      SW<S::NC> cur, alt;
+      sissue(cur, wa);
+      swait(cur);
+      sp_step<D, H1, H2, INV, false, NETS, PERM, false>(v, ld, cur, alt, wa, nullptr, pa,
+                                                        qtab + la * D);
+      st_all(i, std::true_type{});
+      unflip<D>(v);
     }
-    if constexpr (NETS == 2) ld = ld * splat(0.69314718055994531f, T{});  // sum(s) = ln2 * sum(s')
-    if (out) {
-      if constexpr (PIPE) {  // the LDS tile is already the next tile's DMA target
-        const bool al8 = (reinterpret_cast<uintptr_t>(out) & 7) == 0;
-        if (odd) store_rows_direct<D, ROWS, true>(out + row0 * D, v, nrows, al8);
-        else store_rows_direct<D, ROWS, false>(out + row0 * D, v, nrows, al8);
-      } else {
-        if (odd) store_rows<D, ROWS, true>(out + row0 * D, sm, v, nrows, vec);
-        else store_rows<D, ROWS, false>(out + row0 * D, sm, v, nrows, vec);
-      }
+    if constexpr (NETS == 2) ld = ld * splat(0.69314718055994531f, f2{});  // ln2 * sum(s')
+    if constexpr (MODE == kPredict) pair_predict<D>(v, lp);
+  };
+
+  // -------- full tiles: LDS-DMA in, deferred 16-B stores out --------
+  CNF_TR(0);
+#ifdef CNF_SGPR_TRACE
+  if (lane == 0 && gw < 16384)
+    cnf_trace[gw * 8 + 7] = ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
+                            __builtin_amdgcn_s_getreg((31 << 11) | 4);  // XCC_ID, HW_ID
+  int ntr = 0;
+#endif
+  int t = gw;
+  if (t < nfull) wave_dma<D>(sm, a.in + (int64_t)t * TF, lane);
+  f2 pz[D], pld = splat(0.f, f2{});
+  int64_t prow = -1;  // row 2l of the pending (not yet stored) outputs
+  for (; t < nfull; t += nw) {
+    --left;  // tiles after this one
+    if (left >= 3) __builtin_amdgcn_s_setprio(3);
+    else if (left == 2) __builtin_amdgcn_s_setprio(2);
+    else if (left == 1) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA has landed
+    f2 v[D];
+    read_pairs<D>(sm, lane, v);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // rows are in registers
+#ifdef CNF_SGPR_TRACE
+    if (ntr < 2) CNF_TR(1 + 2 * ntr);
+#endif
+    const int64_t row0 = (int64_t)t * kTR;
+    if (prow >= 0) {  // the previous tile's outputs, issued after this tile's reads
+      if (a.out) store_pairs<D>(a.out + prow * D, pz, 2, al);
+      if (a.ld) store_ld2(a.ld + prow, pld, 2, ld8);
     }
-    if (ld_out) store_ld<ROWS>(ld_out, row0, tid, nrows, ld);
-    if (loss_part) {
-      if (odd) tile_loss<D, true>(v, ld, yv, kind, det, lt0, lt1, lt2);
-      else tile_loss<D, false>(v, ld, yv, kind, det, lt0, lt1, lt2);
-    }
+    if (t + nw < nfull) wave_dma<D>(sm, a.in + (int64_t)(t + nw) * TF, lane);
+    Lab lab{};
+    if constexpr (MODE == kLoss) lab = load_labels2<D>(a.y + row0 + 2 * lane, 2, y16);
+    f2 ld;
+    compute(v, ld, row0, 2);
+    if constexpr (MODE == kLoss) pair_loss<D>(v, ld, lab, 2, a.kind, a.det, lt0, lt1, lt2);
+#ifdef CNF_SGPR_TRACE
+    if (ntr < 2) CNF_TR(2 + 2 * ntr);
+    CNF_TR(5);
+    ++ntr;
+#endif
+#pragma unroll
+    for (int k = 0; k < D; ++k) pz[k] = v[k];
+    pld = ld;
+    prow = row0 + 2 * lane;
   }
-  CNF_TL(2);
-  if (loss_part) {
-    if (ticket)  // persistent grid: one hand-off per block, no second launch
-      block_sum3_last<ROWS>(lt0, lt1, lt2, smem, loss_part, ticket, loss_terms, gridDim.x);
-    else
-      block_sum3<ROWS>(lt0, lt1, lt2, smem, loss_part);
+  if (prow >= 0) {
+    if (a.out) store_pairs<D>(a.out + prow * D, pz, 2, al);
+    if (a.ld) store_ld2(a.ld + prow, pld, 2, ld8);
   }
+  // -------- the ragged last tile (B % 128 rows): plain loads, masked stores --------
+  if (t == nfull && nfull < ntiles) {
+    const int64_t row0 = (int64_t)t * kTR;
+    const int64_t r = row0 + 2 * lane;
+    const int nr = r >= B ? 0 : (r + 1 >= B ? 1 : 2);
+    f2 v[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      v[k].x = nr > 0 ? a.in[r * D + k] : 0.f;
+      v[k].y = nr > 1 ? a.in[(r + 1) * D + k] : 0.f;
+    }
+    Lab lab{};
+    if constexpr (MODE == kLoss) lab = load_labels2<D>(a.y + r, nr, false);
+    f2 ld;
+    compute(v, ld, row0, nr);
+    if constexpr (MODE == kLoss) pair_loss<D>(v, ld, lab, nr, a.kind, a.det, lt0, lt1, lt2);
+    if (a.out) store_pairs<D>(a.out + r * D, v, nr, 4);
+    if (a.ld) store_ld2(a.ld + r, ld, nr, false);
+  }
+  CNF_TR(6);
+  if constexpr (MODE == kLoss) block_sum3<kWaves * 64>(lt0, lt1, lt2, smem, a.part);
 }
 
-using KFn = void (*)(const float*, const int32_t*, const int32_t*, const float*, float*, float*,
-                     float*, int64_t, int, int, int, int, int, const int64_t*, float*, int, float,
-                     unsigned*, float*);
+using KFn = void (*)(const float*, const int32_t*, const int32_t*, const float*, KArgs);
 
-constexpr int kRW = 2, kRows = 256;
+// variants without permutation: fwd, inv, loss, predict, fwd+all, inv+all;
+// with a random_flip permutation: fwd, inv, fwd+all, inv+all
+enum Var { vFwd, vInv, vLoss, vPredict, vFwdAll, vInvAll, kNVar };
 
 struct SEntry {
   int D, H1, H2;
-  KFn fn[3][2][2];  // [pipe][nets - 1][inverse]
+  KFn fn[2][kNVar];  // [nets - 1][variant]
+  KFn pfn[2][4];     // [nets - 1][fwd, inv, fwd+all, inv+all] with permutation
 };
 
-#define CNF_SGPR_P(D, H1, H2, P)                                                      \
-  {{k_sgpr<D, H1, H2, false, 1, kRW, kRows, P>, k_sgpr<D, H1, H2, true, 1, kRW, kRows, P>}, \
-   {k_sgpr<D, H1, H2, false, 2, kRW, kRows, P>, k_sgpr<D, H1, H2, true, 2, kRW, kRows, P>}}
+#define CNF_SV(D, H1, H2, N)                                                                  \
+  {k_sgpr<D, H1, H2, N, kFwd, false, false>, k_sgpr<D, H1, H2, N, kInv, false, false>,         \
+   k_sgpr<D, H1, H2, N, kLoss, false, false>, k_sgpr<D, H1, H2, N, kPredict, false, false>,    \
+   k_sgpr<D, H1, H2, N, kFwd, true, false>, k_sgpr<D, H1, H2, N, kInv, true, false>}
+#define CNF_SP(D, H1, H2, N)                                                                  \
+  {k_sgpr<D, H1, H2, N, kFwd, false, true>, k_sgpr<D, H1, H2, N, kInv, false, true>,           \
+   k_sgpr<D, H1, H2, N, kFwd, true, true>, k_sgpr<D, H1, H2, N, kInv, true, true>}
 #define CNF_SGPR(D, H1, H2) \
-  {D, H1, H2, {CNF_SGPR_P(D, H1, H2, 0), CNF_SGPR_P(D, H1, H2, 1), CNF_SGPR_P(D, H1, H2, 2)}}
+  {D, H1, H2, {CNF_SV(D, H1, H2, 1), CNF_SV(D, H1, H2, 2)}, {CNF_SP(D, H1, H2, 1), CNF_SP(D, H1, H2, 2)}}
 
 // every shape of the VALU table whose Linears fit the 32-float buffer
 const SEntry kSTable[] = {
+#ifdef CNF_SGPR_DEV  // development builds: the headline shape only
+    CNF_SGPR(10, 5, 5),
+#else
     CNF_SGPR(2, 5, 5), CNF_SGPR(3, 5, 5), CNF_SGPR(4, 5, 5), CNF_SGPR(5, 5, 5),
     CNF_SGPR(6, 5, 5), CNF_SGPR(8, 5, 5), CNF_SGPR(10, 5, 5),
     CNF_SGPR(3, 3, 3), CNF_SGPR(8, 3, 3), CNF_SGPR(10, 3, 3),
     CNF_SGPR(3, 3, 0), CNF_SGPR(3, 0, 0), CNF_SGPR(10, 0, 0),
     CNF_SGPR(10, 5, 0), CNF_SGPR(3, 5, 0),
+#endif
 };
 
 const SEntry* find(const Shape& s) {
@@ -394,50 +636,16 @@ const SEntry* find(const Shape& s) {
   return nullptr;
 }
 
-}  // namespace
+size_t lds_bytes(const Shape& s) { return (size_t)kWaves * kTR * s.D * 4; }
 
-// all_outputs (z_all) launches stay on k_valu: the per-layer stores cost this
-// kernel SGPRs it does not have.
-bool sgpr_enabled(const Shape& s) {
-  if (!s.sp_ok || s.strict || !s.shift || !find(s)) return false;
-  const char* e = std::getenv("CNF_SGPR");  // A/B switch: CNF_SGPR=0 keeps k_valu
-  return !(e && e[0] == '0');
-}
-
-// A/B switch CNF_SGPR_PIPE: 0 one tile per block, 1 block-wide DMA, 2 per-wave
-// DMA (default).  A wave-granular dynamic schedule (atomic unit counters per
-// XCD, per-unit loss records) was measured and dropped: 24% slower at 1M rows,
-// no faster at 8M.
-static int pipe_mode() {
-  const char* e = std::getenv("CNF_SGPR_PIPE");
-  if (e && e[0] >= '0' && e[0] <= '2') return e[0] - '0';
-  return 2;
-}
-static bool pipe_on() { return pipe_mode() != 0; }
-// A/B switch CNF_SGPR_PRIO (default on): s_setprio by tiles remaining on the
-// persistent grid.  The SIMD's oldest-first arbitration otherwise finishes
-// blocks far apart (tools/timeline.py: 97..231 us at 8M rows) and idles
-// through the tail; measured -4 % at 8M rows, neutral at 1M.  (Non-temporal
-// output stores were measured too: +27 % at 1M, dropped.)
-static bool prio_on() {
-  const char* e = std::getenv("CNF_SGPR_PRIO");
-  return !(e && e[0] == '0');
-}
-
-static size_t lds_bytes(const Shape& s, bool pipe) {
-  size_t lds = (size_t)kRW * kRows * s.D * 4;
-  if (lds < (size_t)3 * kRows * 4 + 4 * 65) lds = (size_t)3 * kRows * 4 + 4 * 65;
-  return lds;
-}
-
-static int resident(KFn fn, size_t lds) {
+int resident_blocks(KFn fn, size_t lds) {
   static std::mutex mu;
   static std::unordered_map<const void*, int> cache;
   std::lock_guard<std::mutex> g(mu);
   auto it = cache.find((const void*)fn);
   if (it != cache.end()) return it->second;
   int n = 0, dev = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kRows, lds) != hipSuccess || n < 1)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kWaves * 64, lds) != hipSuccess || n < 1)
     n = 1;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
@@ -447,62 +655,73 @@ static int resident(KFn fn, size_t lds) {
   return n * cus;
 }
 
-static KFn pick(const SEntry* e, const Shape& s, bool inverse, bool pipe) {
-  return e->fn[pipe ? pipe_mode() : 0][s.scale ? 1 : 0][inverse ? 1 : 0];
-}
-
-static int64_t blocks_dir(const Shape& s, int64_t B, bool inverse) {
-  const int64_t ntiles = (B + kRW * kRows - 1) / (kRW * kRows);
-  const SEntry* e = find(s);
-  if (!e || !pipe_on()) return ntiles;
-  int cap = resident(pick(e, s, inverse, true), lds_bytes(s, true));
-  if (const char* g = std::getenv("CNF_SGPR_GRID")) {  // experiment: fixed grid cap
-    const int n = std::atoi(g);
-    if (n > 0) cap = n;
+KFn pick(const SEntry* e, const Shape& s, int mode, bool all) {
+  const int n = s.scale ? 1 : 0;
+  if (s.any_perm) {
+    if (mode == kLoss || mode == kPredict) return nullptr;  // k_valu handles these
+    return e->pfn[n][(mode == kInv ? 1 : 0) + (all ? 2 : 0)];
   }
-  if (ntiles <= cap) return ntiles;
-  // balanced: the smallest grid that still gives every block the same tile
-  // count (1M rows: 2,048 tiles on 1,024 blocks x 2, not 1,280 blocks x 1-2)
-  // (measured slower: 4 waves/SIMD hide less than 5, so it stays opt-in)
-  const char* b = std::getenv("CNF_SGPR_BAL");  // A/B switch: 1 = balanced grid
-  if (!(b && b[0] == '1')) return cap;
-  const int64_t per = (ntiles + cap - 1) / cap;
-  return (ntiles + per - 1) / per;
+  if (all) return e->fn[n][mode == kInv ? vInvAll : vFwdAll];
+  return e->fn[n][mode];
 }
 
-int64_t sgpr_blocks(const Shape& s, int64_t B) { return blocks_dir(s, B, false); }
+int64_t grid_for(KFn fn, const Shape& s, int64_t B) {
+  const int64_t ntiles = (B + kTR - 1) / kTR;
+  const int64_t want = (ntiles + kWaves - 1) / kWaves;
+  const int64_t cap = resident_blocks(fn, lds_bytes(s));
+  return want < cap ? want : cap;
+}
+
+bool io_ok(const void* p, int64_t align) {
+  return p == nullptr || (reinterpret_cast<uintptr_t>(p) % align) == 0;
+}
+
+}  // namespace
+
+// Shapes this kernel serves: shift on (NICE keeps s = 0), non-strict, every
+// Linear fits 32 floats, and the row batch in HBM is 16-B aligned (the LDS-DMA
+// reads whole 16-B words; misaligned views stay on k_valu).
+bool sgpr_enabled(const Shape& s) {
+  return s.sp_ok && !s.strict && s.shift && find(s) && !(s.options & CNF_OPT_NO_SGPR);
+}
+
+int64_t sgpr_blocks(const Shape& s, int64_t B) {
+  const SEntry* e = find(s);
+  KFn fn = e ? pick(e, s, kLoss, false) : nullptr;
+  return fn ? grid_for(fn, s, B) : 0;
+}
 
 int sgpr_run(const Shape& s, const void* prepared, const float* in, float* out, float* ld,
              float* all, int64_t B, bool inverse, hipStream_t st, const int64_t* y,
-             float* loss_ws, int kind, float det, float* loss_terms) {
+             float* loss_ws, int kind, float det, float* loss_terms, const float* log_priors) {
   const SEntry* e = find(s);
-  if (!e || !s.sp_ok || all) return CNF_ERR_UNSUPPORTED;  // every-layer outputs: k_valu
+  if (!e || !sgpr_enabled(s)) return CNF_ERR_UNSUPPORTED;
   if (B == 0) return CNF_OK;
+  if ((B + kTR - 1) / kTR > 0x7fffffffLL) return CNF_ERR_UNSUPPORTED;
+  if (!io_ok(in, 16) || !io_ok(out, 4) || !io_ok(all, 16) || !io_ok(ld, 4)) return CNF_ERR_UNSUPPORTED;
+  const int mode = log_priors ? kPredict : (loss_ws ? kLoss : (inverse ? kInv : kFwd));
+  KFn fn = pick(e, s, mode, all != nullptr);
+  if (!fn) return CNF_ERR_UNSUPPORTED;
   const char* base = static_cast<const char*>(prepared);
   const int32_t* fwd_q = reinterpret_cast<const int32_t*>(base);
   const int32_t* inv_q = fwd_q + s.L * s.D;
   const int32_t* flags = inv_q + s.L * s.D;
   const float* W = reinterpret_cast<const float*>(base + idx_bytes(s)) + s.sp_region;
-  auto al = [](const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
-  const int vec = al(in) && al(out) && al(all);
-  // the inverse takes the persistent LDS-DMA form too since the weight loads became
-  // compiler-visible (118 VGPRs, 4 waves/SIMD, no spills): -8 % on cfg5.
-  // A/B switch CNF_SGPR_INV_PIPE=0 keeps one tile per block.
-  const char* ip = std::getenv("CNF_SGPR_INV_PIPE");
-  const bool pipe = pipe_on() && (!inverse || !(ip && ip[0] == '0'));
-  KFn fn = pick(e, s, inverse, pipe);
-  const int64_t nblk = pipe ? blocks_dir(s, B, inverse) : (B + kRW * kRows - 1) / (kRW * kRows);
-  const size_t lds = lds_bytes(s, pipe);
-  // one-launch loss hand-off on the persistent grid (workspace ticket word,
-  // zeroed by the caller once; the last block resets it)
-  const char* lt = std::getenv("CNF_LOSS_TICKET");
-  const bool fused = loss_ws && pipe && lt && lt[0] == '1';  // measured slower: off
-  hipLaunchKernelGGL(fn, dim3((unsigned)nblk), dim3(kRows), lds, st, W, inverse ? inv_q : fwd_q,
-                     flags, in, out, ld, all, B, s.L, prio_on() ? 1 : 0, 0,
-                     s.any_perm ? 1 : 0, vec,
-                     y, loss_ws ? loss_ws + 4 : nullptr, kind, det,
-                     fused ? reinterpret_cast<unsigned*>(loss_ws) : nullptr, loss_terms);
-  if (loss_ws && !fused) reduce_partials(loss_ws + 4, (int)nblk, 4, 0, nullptr, loss_terms, st);
+  KArgs a{};
+  a.in = in;
+  a.out = out;
+  a.ld = ld;
+  a.all = all;
+  a.y = y;
+  a.part = loss_ws ? loss_ws + 4 : nullptr;
+  a.B = B;
+  a.L = s.L;
+  a.kind = kind;
+  a.det = det;
+  const int64_t nblk = grid_for(fn, s, B);
+  hipLaunchKernelGGL(fn, dim3((unsigned)nblk), dim3(kWaves * 64), lds_bytes(s), st, W,
+                     inverse ? inv_q : fwd_q, flags, log_priors, a);
+  if (mode == kLoss) reduce_partials(loss_ws + 4, (int)nblk, 4, 0, nullptr, loss_terms, st);
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) {
     set_hip_error(err);
@@ -513,12 +732,10 @@ int sgpr_run(const Shape& s, const void* prepared, const float* in, float* out, 
 
 }  // namespace cnf
 
-#ifdef CNF_TIMELINE
-extern "C" int cnf_diag_timeline(unsigned long long* host, int n) {
-  if (n > 4096 * 4) n = 4096 * 4;
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(cnf_tl), n * 8, 0, hipMemcpyDeviceToHost) ==
-                 hipSuccess
-             ? n
-             : -1;
+#ifdef CNF_SGPR_TRACE
+extern "C" int cnf_diag_trace(unsigned long long* host, int n) {
+  if (n > 16384 * 8) n = 16384 * 8;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(cnf_trace), (size_t)n * 8, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? n : -1;
 }
 #endif

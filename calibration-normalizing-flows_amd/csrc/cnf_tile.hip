@@ -230,7 +230,7 @@ struct PrepSeg {
   int64_t dst;  // float offset in the weights region
   int mode;     // 0: natural copy, 1: MFMA tiles, 2: compact (VALU), 3: packed (SGPR)
   int nout_full, nin_full, in_off, nin, nout, OT, KS;
-  float mul;  // mode 3: weights and bias scaled by this (log2 e on the s-net's last Linear)
+  float wmul, bmul;  // mode 3: weights / bias scale (relu clamp 2^-64, log2 e; cnf_sgpr.hip)
 };
 
 struct PrepArgs {
@@ -264,10 +264,10 @@ __global__ void k_prepare(PrepArgs a, float* __restrict__ wreg, int32_t* __restr
       float v = 0.f;
       const int o = (int)(i / S), j = (int)(i - (int64_t)o * S);
       if (o < g.nout) {
-        if (j == 1) v = g.b[o] * g.mul;
+        if (j == 1) v = g.b[o] * g.bmul;
         else if (j == 0 || j <= g.nin) {
           const int k = j == 0 ? 0 : j - 1;
-          v = g.W[(int64_t)o * g.nin_full + g.in_off + k] * g.mul;
+          v = g.W[(int64_t)o * g.nin_full + g.in_off + k] * g.wmul;
         }
       }
       dst[i] = v;
@@ -426,9 +426,17 @@ int prepare_run(const Shape& s, const float* const* params, void* prepared, hipS
         PrepSeg& g = b.seg[k];
         const int i = k % s.n_lin;
         g.mode = 3;
-        g.nout = i == s.n_lin - 1 ? s.DT : g.nout_full;
-        // the s-net (first net when scale is on) ends in log2(e) * s
-        g.mul = (s.scale && k / s.n_lin == 0 && i == s.n_lin - 1) ? 1.4426950408889634f : 1.f;
+        const bool last = i == s.n_lin - 1;
+        g.nout = last ? s.DT : g.nout_full;
+        // k_sgpr folds relu into the clamp bit: hidden outputs are kept scaled
+        // by 2^-64 (so relu(a) 2^-64 = clamp(a 2^-64, 0, 1)) and the next
+        // Linear's input columns undo it; the s-net (first net when scale is
+        // on) ends in log2(e) * s.  Powers of two: exact.
+        const float sin = i == 0 ? 1.f : 0x1p-64f;
+        float sout = last ? 1.f : 0x1p-64f;
+        if (s.scale && k / s.n_lin == 0 && last) sout *= 1.4426950408889634f;
+        g.wmul = sout / sin;
+        g.bmul = sout;
         g.dst = d2 + (k / s.n_lin) * s.sp_net_floats + s.sp_lin_off[i];
       }
       hipLaunchKernelGGL(k_prepare, dim3(b.nseg), dim3(256), 0, st, b, wreg, idx);

@@ -240,20 +240,6 @@ const Entry kTable[] = {
     CNF_VALU(10, 7, 0), CNF_VALU(10, 5, 0), CNF_VALU(3, 5, 0),
 };
 
-// A/B variants of the headline shape (CNF_VALU_VARIANT=i, D=10, hidden=[5,5]):
-// rows per lane, threads per block, persistent grid, waves-per-SIMD bound.
-const Variant kExp[] = {
-    CNF_VARIANT(10, 5, 5, 1, 256, false, 6, false, false),                // 0: libm exp
-    CNF_VARIANT(10, 5, 5, 1, 256, false, 6, true, false),                 // 1: = large
-    CNF_VARIANT(10, 5, 5, 2, 256, false, 4, true, true),                  // 2: = small
-    CNF_VARIANT_X(10, 5, 5, 2, 256, false, 4, true, false, false, true),  // 3: chunked, 2/lane
-    CNF_VARIANT(10, 5, 5, 4, 256, false, 2, true, true),                  // 4: LDS, 4/lane
-    CNF_VARIANT(10, 5, 5, 2, 256, false, 4, true, false),                 // 5: scalar, 2/lane
-    CNF_VARIANT(10, 5, 5, 2, 128, false, 4, true, true),                  // 6: LDS, 2/lane, 128 thr
-    CNF_VARIANT(10, 5, 5, 1, 256, false, 6, true, true),                  // 7: LDS, 1/lane
-    CNF_VARIANT_Y(10, 5, 5, 2, 256, false, 4, true, true, false, false, true),  // 8: LDS pairs
-};
-
 int cu_count() {
   static int n = [] {
     int dev = 0, v = 0;
@@ -293,13 +279,7 @@ static const Variant* pick_variant(const Shape& s, int64_t B) {
   const Entry& e = kTable[s.valu_id];
   const bool lds_fits =
       (size_t)256 * 2 * s.D * 4 + (size_t)s.L * s.nets * s.valu_net_floats * 4 <= 64 * 1024;
-  const Variant* var = (B > kLargeBatch || !lds_fits) ? &e.large : &e.small;
-  const char* xv = std::getenv("CNF_VALU_VARIANT");
-  if (xv && e.D == 10 && e.H1 == 5 && e.H2 == 5) {
-    const int k = std::atoi(xv);
-    if (k >= 0 && k < (int)(sizeof(kExp) / sizeof(kExp[0]))) var = &kExp[k];
-  }
-  return var;
+  return (B > kLargeBatch || !lds_fits) ? &e.large : &e.small;
 }
 
 static int64_t blocks_for(const Shape& s, const Variant* var, KFn fn, int64_t B) {
@@ -312,11 +292,17 @@ static int64_t blocks_for(const Shape& s, const Variant* var, KFn fn, int64_t B)
   return nblk;
 }
 
+// Loss partial records a fused eval may write: whichever of k_sgpr / k_valu
+// serves the launch (k_valu takes misaligned views and permuted stacks).
 int valu_loss_blocks(const Shape& s, int64_t B) {
   if (s.valu_id < 0) return -1;
-  if (sgpr_enabled(s)) return (int)sgpr_blocks(s, B);
   const Variant* var = pick_variant(s, B);
-  return (int)blocks_for(s, var, var->fn[0][s.strict ? 1 : 0], B);
+  int64_t n = blocks_for(s, var, var->fn[0][s.strict ? 1 : 0], B);
+  if (sgpr_enabled(s)) {
+    const int64_t m = sgpr_blocks(s, B);
+    if (m > n) n = m;
+  }
+  return (int)n;
 }
 
 int valu_run(const Shape& s, const void* prepared, const float* in, float* out, float* ld,
@@ -324,9 +310,11 @@ int valu_run(const Shape& s, const void* prepared, const float* in, float* out, 
              float* loss_ws, int kind, float det, float* loss_terms) {
   if (s.valu_id < 0) return CNF_ERR_UNSUPPORTED;
   if (B == 0) return CNF_OK;
-  if (sgpr_enabled(s) && !all)
-    return sgpr_run(s, prepared, in, out, ld, all, B, inverse, st, y, loss_ws, kind, det,
-                    loss_terms);
+  if (sgpr_enabled(s)) {
+    const int r = sgpr_run(s, prepared, in, out, ld, all, B, inverse, st, y, loss_ws, kind, det,
+                           loss_terms);
+    if (r != CNF_ERR_UNSUPPORTED) return r;
+  }
   const Entry& e = kTable[s.valu_id];
   if (e.nf != s.valu_net_floats) return CNF_ERR_DESC;  // host/device layout disagree
   const Variant* var = pick_variant(s, B);

@@ -119,19 +119,11 @@ __device__ __forceinline__ void linear(const WP* __restrict__ w, const T* x, T* 
   constexpr int S = Lin<NIN, NOUTF>::stride;
 #pragma unroll
   for (int o = 0; o < NOUT; ++o) {
-#ifdef CNF_DIAG_FAKE_WEIGHTS
-    T a = splat(0.001f * o, T{});
-#else
     T a = splat(wld(w, NOUTF * S + o), T{});
-#endif
     if constexpr (POISON) a += p0;
 #pragma unroll
     for (int k = 0; k < NIN; ++k) {
-#ifdef CNF_DIAG_FAKE_WEIGHTS  // diagnostic build only: weights as literals (no loads)
-      a = fmaT(0.01f * (float)(o * 7 + k + 1) + 1e-4f * S, x[k], a);
-#else
       a = fmaT(wld(w, o * S + k), x[k], a);
-#endif
     }
     y[o] = RELU ? relu<STRICT>(a) : a;
   }

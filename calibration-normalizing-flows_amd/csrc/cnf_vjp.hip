@@ -237,7 +237,11 @@ __global__ __launch_bounds__(kVRows) void k_vjp(
 #pragma unroll
         for (int j = 0; j < D; ++j) se += expf(z[j] - m);
         const float lse = m + logf(se);
-        const int yy = valid ? (int)y[row] : 0;
+        // a label outside [0, D) poisons this row's loss and gradient with NaN
+        // (the reference's probs.gather raises on it)
+        const int64_t yr = valid ? y[row] : 0;
+        const bool yok = yr >= 0 && yr < D;
+        const int yy = yok ? (int)yr : 0;
         float zy = z[0];
 #pragma unroll
         for (int j = 1; j < D; ++j) zy = (j == yy) ? opaque(z[j]) : zy;
@@ -255,6 +259,7 @@ __global__ __launch_bounds__(kVRows) void k_vjp(
           coef = 1.f;
           gld = -det * grad_scale;
         }
+        if (!yok) ce_term = loss_row = coef = __builtin_nanf("");
 #pragma unroll
         for (int j = 0; j < D; ++j) {
           const float p = expf(z[j] - lse);
@@ -580,9 +585,7 @@ int reduce_partials(const float* partials, int nblk, int PS, int P, float* grads
   if (P > 0)
     hipLaunchKernelGGL(k_reduce_cols, dim3((unsigned)((P + 63) / 64)), dim3(256), 0, st,
                        partials, nblk, PS, P, grads);
-  const char* e = std::getenv("CNF_REDUCE4");  // A/B switch: 0 = one-wave k_reduce_rows
-  const bool r4 = PS == 4 && P == 0 && (reinterpret_cast<uintptr_t>(partials) & 15) == 0 &&
-                  !(e && e[0] == '0');
+  const bool r4 = PS == 4 && P == 0 && (reinterpret_cast<uintptr_t>(partials) & 15) == 0;
   if (terms && r4)
     hipLaunchKernelGGL(k_reduce_rows4, dim3(1), dim3(kRR), 0, st,
                        reinterpret_cast<const float4*>(partials), nblk, terms);

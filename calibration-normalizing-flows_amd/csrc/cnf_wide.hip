@@ -434,9 +434,7 @@ int64_t wide_layer_floats(const Shape& s) {
 // Final-output forward / inverse of shift-on, non-strict stacks in the table;
 // every-layer outputs and strict_nan stay on k_tile.
 bool wide_ok(const Shape& s) {
-  if (!wfind(s) || !s.shift || s.strict) return false;
-  const char* e = std::getenv("CNF_WIDE");  // A/B switch: CNF_WIDE=0 keeps k_tile
-  return !(e && e[0] == '0');
+  return wfind(s) && s.shift && !s.strict && !(s.options & CNF_OPT_NO_WIDE);
 }
 
 int wide_prepare(const Shape& s, const float* const* params, void* prepared, hipStream_t st) {

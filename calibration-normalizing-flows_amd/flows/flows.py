@@ -88,6 +88,9 @@ class Flow(nn.Module):
         # a flow is computationally invertible iff every layer is
         self.invertible = all(ly.invertible for ly in self.layers)
         self.strict_nan = kwargs.get("strict_nan", None)
+        # cnf_desc.options bits (cnf_hip._lib.OPT_*): keep launches off a kernel
+        # family, for A/B runs and tests; 0 = the fastest kernel
+        self.native_options = int(kwargs.get("native_options", 0))
         self._stack = None
         self._stack_key = None
 
@@ -100,12 +103,23 @@ class Flow(nn.Module):
 
     # -- native plumbing --------------------------------------------------
     def _native_stack(self):
-        key = (tuple(id(ly) for ly in self.layers), self._strict())
+        key = (tuple(id(ly) for ly in self.layers), self._strict(), self.native_options)
         if self._stack is None or self._stack_key != key:
             from cnf_hip.engine import CouplingStack
-            self._stack = CouplingStack(list(self.layers), strict_nan=self._strict())
+            self._stack = CouplingStack(list(self.layers), strict_nan=self._strict(),
+                                        options=self.native_options)
             self._stack_key = key
         return self._stack
+
+    def invalidate_native(self):
+        """Drop the native binding's prepared weights.  Needed only after writes
+        that bypass torch's version counters (`p.data.copy_(...)`); optimizer
+        steps, `load_state_dict` and in-place ops are tracked automatically."""
+        self._stack = None
+        self._stack_key = None
+        for ly in self.layers:
+            if isinstance(ly, NvpCouplingLayer):
+                ly._stack = None
 
     def _strict(self):
         return STRICT_NAN if self.strict_nan is None else bool(self.strict_nan)
@@ -119,7 +133,9 @@ class Flow(nn.Module):
         try:
             if _needs_grad(x, self):
                 if inverse:
-                    return None  # autograd through the inverse: per-layer path
+                    # no native reverse mode of the inverse: the reference's ops
+                    _not_native("autograd through the inverse (Flow.backward)")
+                    return None
                 out, ld = stack.forward_autograd(x, want_all=want_all)
             else:
                 fin, ld, allt = stack.run(x, inverse=inverse, want_all=want_all)
@@ -250,6 +266,7 @@ class NvpCouplingLayer(nn.Module):
         try:
             if _needs_grad(x, self):
                 if inverse:
+                    _not_native("autograd through the inverse (NvpCouplingLayer.backward)")
                     return None
                 z, ld = self._stack.forward_autograd(x, want_all=False)
             else:

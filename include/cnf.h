@@ -60,11 +60,16 @@ typedef struct cnf_desc {
   int32_t shift;                /* 1: t-net present; 0: t == 0                    */
   int32_t strict_nan;           /* 1: reproduce the reference's inf*0 = NaN at
                                    masked positions (flows/flows.py:107,123)      */
-  int32_t reserved;
+  int32_t options;              /* CNF_OPT_* bits (0: pick the fastest kernel)    */
   const int64_t* perms;         /* HOST pointer, NULL or L*D entries: layer l's
                                    random_flip permutation (flows/flows.py:92-99);
                                    a row whose first entry is < 0 = no perm      */
 } cnf_desc;
+
+/* cnf_desc.options: keep a launch off a kernel family (A/B and test use;
+ * results agree to fp32 rounding either way). */
+#define CNF_OPT_NO_SGPR 1   /* narrow flows: k_valu instead of k_sgpr          */
+#define CNF_OPT_NO_WIDE 2   /* wide flows: k_tile instead of k_wide            */
 
 /* One float per parameter, in the reference's state_dict order. */
 int cnf_param_count(const cnf_desc* desc, int64_t* n_floats);
@@ -117,6 +122,17 @@ int cnf_forward_loss(const cnf_desc* desc, const void* prepared, const float* x,
                      float* loss_terms, int64_t B, void* workspace, size_t workspace_bytes,
                      void* stream);
 
+/* Fused calibrated prediction: Calibrator.predict of the flow calibrator
+ * (calibrators.py:40-44 with TorchFlowCalibrator.predict_post, :330-353), per row
+ *   p = softmax(flow(x - mean(x))),  probs = softmax(log(p + 1e-7) - log_priors)
+ *   log_priors [D]     DEVICE pointer (the calibrator's log class priors)
+ *   probs      [B][D]  calibrated probabilities
+ *   logdet     [B]     log-det of the centred rows, may be NULL
+ * Narrow flows (the k_sgpr shapes) without random_flip; CNF_ERR_UNSUPPORTED
+ * otherwise (the caller composes cnf_forward with its own softmax). */
+int cnf_predict(const cnf_desc* desc, const void* prepared, const float* x,
+                const float* log_priors, float* probs, float* logdet, int64_t B, void* stream);
+
 /* Workspace bytes cnf_vjp / cnf_loss_vjp need for a batch of B rows. */
 int cnf_vjp_workspace_bytes(const cnf_desc* desc, int64_t B, size_t* bytes);
 
@@ -147,9 +163,11 @@ int cnf_loss_vjp(const cnf_desc* desc, const void* prepared, const float* x,
                  float* loss_terms, float* grads, float* dx, int64_t B, void* workspace,
                  size_t workspace_bytes, void* stream);
 
-/* Which kernel family serves this descriptor's final-output launches:
- * "sgpr-fused" (pipelined scalar weights), "valu-fused" (every-layer outputs,
- * strict_nan, and shapes whose Linears exceed 32 floats), "mfma-tile" (wide). */
+/* Which kernel family serves this descriptor's launches: "sgpr-fused"
+ * (pipelined scalar weights, every output mode), "valu-fused" (strict_nan,
+ * shapes whose Linears exceed 32 floats, misaligned views), "mfma-wide"
+ * (register-resident MFMA, the wide shapes of its table), "mfma-tile" (other
+ * wide shapes, every-layer outputs of wide stacks). */
 const char* cnf_kernel_name(const cnf_desc* desc);
 
 const char* cnf_strerror(int status);

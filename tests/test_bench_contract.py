@@ -37,3 +37,40 @@ def test_nice_has_no_scale_flops():
     # scale=False: one net, shift-only update (flows/flows.py:76-79)
     per_layer = 2 * (2 * 5 + 5 * 5 + 5 * 1) + 1
     assert bench.algo_flops_per_vec(3, 2, [5, 5], scale=False) == 2 * per_layer
+
+
+def test_roofline_names_the_binding_roof():
+    # cfg2 fused loss pass: 92 B and 1,890 flops per vector -> the VALU roof
+    # (83.2 G vec/s) binds before HBM (87.0 G vec/s); SURVEY 8(d)
+    r = bench.roofline(1 << 20, 92, 1890, 42.9e-6)
+    assert r["bound"] == "valu" and r["unit"] == "TFLOP/s"
+    rate = (1 << 20) / 42.9e-6
+    assert abs(r["frac"] - rate / (157.3e12 / 1890)) < 1e-4
+    assert abs(r["compute_frac"] - r["frac"]) < 1e-4
+    # every-layer outputs (284 B) are HBM-bound
+    r = bench.roofline(1 << 20, 284, 1890, 70e-6)
+    assert r["bound"] == "hbm" and abs(r["frac"] - r["hbm_frac"]) < 1e-4
+    # cfg4 is MFMA-bound
+    assert bench.roofline(1 << 18, 804, 961800, 3e-3, mfma=True)["bound"] == "mfma"
+
+
+def test_gpus_flag_self_launches_ranks():
+    """`bench.py --gpus 2` with no launcher starts two rank processes itself
+    (here with --launch-check: gloo wiring only, no GPU)."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                          "--launch-check"], env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = json.loads(out.stdout.strip().splitlines()[-1])
+    assert line == {"n_gpus": 2, "rank_sum": 1.0}
+
+
+def test_gpus_flag_must_match_launcher_world():
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1",
+                          "--launch-check"], env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode != 0 and "WORLD_SIZE=2" in out.stderr

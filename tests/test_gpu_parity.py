@@ -219,7 +219,7 @@ def test_fused_forward_loss_matches_oracle(kind):
     (100, 3, [], False, False),          # NICE, no hidden layer
     (32, 4, [64, 64], True, True),       # mid width, one partial state tile
 ])
-def test_wide_kernel_matches_oracle_and_tile(D, L, hidden, flip, scale, monkeypatch):
+def test_wide_kernel_matches_oracle_and_tile(D, L, hidden, flip, scale):
     """k_wide (cnf_wide.hip): register-resident MFMA path against the numpy
     oracle, the round trip, and the LDS-tile kernel it replaces."""
     flow = _make_flow(D, L, hidden, 0.05, 21, random_flip=flip, scale=scale)
@@ -237,8 +237,163 @@ def test_wide_kernel_matches_oracle_and_tile(D, L, hidden, flip, scale, monkeypa
     assert rel_err(ld.cpu().numpy(), old) <= TOL
     assert ((xr - x).abs() / (x.abs() + 1)).max().item() <= TOL
     assert ((ild + ld).abs() / (ld.abs() + 1)).max().item() <= TOL
-    monkeypatch.setenv("CNF_WIDE", "0")          # the k_tile path, same prepared blob
+    from cnf_hip import _lib
+    flow.native_options = _lib.OPT_NO_WIDE        # the k_tile path
+    assert flow._native_stack().kernel_name() == "mfma-tile"
     with torch.no_grad():
         zt, ldt = flow.transform(x)
     assert rel_err(z.cpu().numpy(), zt.cpu().numpy()) <= TOL
     assert rel_err(ld.cpu().numpy(), ldt.cpu().numpy()) <= TOL
+
+
+@pytest.mark.parametrize("name", [n for n in CASES if n != "g6_d4_nan"])
+def test_final_only_inverse_matches_reference_fixture(name):
+    """inverse_transform (final x and log-det only -- the cfg5 launch, k_sgpr
+    for the narrow shapes) against the reference's Flow.backward fixture
+    (flows/flows.py:27-37, 114-126)."""
+    meta, state, d = load(name)
+    if "inv_xs" not in d:
+        pytest.skip("no inverse recorded")
+    flow = build_flow(meta, state, DEV)
+    z = torch.from_numpy(d["zs"][-1]).to(DEV)
+    n0 = engine.stats["inverse"]
+    with torch.no_grad():
+        x, ld = flow.inverse_transform(z)
+    assert engine.stats["inverse"] == n0 + 1, "native cnf_inverse did not run"
+    tol = max(TOL, 2 * _fp32_floor(meta, state, d))
+    assert rel_err(x.cpu().numpy(), d["inv_xs"][-1]) <= tol
+    assert tuple(ld.shape) == d["inv_ld"].shape
+    assert rel_err(ld.cpu().numpy(), d["inv_ld"]) <= tol
+
+
+@pytest.mark.parametrize("name", [n for n in CASES if n not in ("g6_d4_nan",)])
+def test_valu_family_matches_reference_fixture(name):
+    """k_valu (the fallback family: misaligned views, permuted loss) held to the
+    same fixtures once k_sgpr is switched off (cnf_desc.options)."""
+    from cnf_hip import _lib
+    meta, state, d = load(name)
+    if meta["D"] > 16:
+        pytest.skip("wide shape")
+    flow = build_flow(meta, state, DEV)
+    flow.native_options = _lib.OPT_NO_SGPR
+    if flow._native_stack().kernel_name() != "valu-fused":
+        pytest.skip("shape outside the k_valu table")
+    x = torch.from_numpy(d["x"]).to(DEV)
+    with torch.no_grad():
+        zs, ld = flow(x)
+        z, ld2 = flow.transform(x)
+    assert rel_err(torch.stack(zs).cpu().numpy(), d["zs"]) <= TOL
+    assert rel_err(ld.cpu().numpy(), d["ld"]) <= TOL
+    assert rel_err(z.cpu().numpy(), d["zs"][-1]) <= TOL
+    if "inv_xs" in d:
+        with torch.no_grad():
+            xr, ild = flow.inverse_transform(torch.from_numpy(d["zs"][-1]).to(DEV))
+        tol = max(TOL, 2 * _fp32_floor(meta, state, d))
+        assert rel_err(xr.cpu().numpy(), d["inv_xs"][-1]) <= tol
+
+
+def test_every_layer_outputs_at_full_size():
+    """The zs list (every layer's z, 284 B/row) at 2^20 rows with random_flip:
+    its last entry is bitwise the final-only output, log-dets agree."""
+    flow = _make_flow(10, 6, [5, 5], 0.1, 5, random_flip=True)
+    x = _logits((1 << 20) + 33, 10, 7)
+    with torch.no_grad():
+        zs, ld = flow(x)
+        z, ld2 = flow.transform(x)
+        xs, ild = flow.backward(z)
+    assert len(zs) == 6 and torch.equal(zs[-1], z) and torch.equal(ld, ld2)
+    assert ((xs[-1] - x).abs() / (x.abs() + 1)).max().item() <= TOL
+    assert ((ild + ld).abs() / (ld.abs() + 1)).max().item() <= TOL
+    idx = torch.randperm(x.shape[0], generator=torch.Generator().manual_seed(2))[:1024].to(DEV)
+    ol = _oracle_layers(flow)
+    for l, ly in enumerate(flow.layers):
+        ol[l] = O.OracleLayer(10, ol[l].s_net, ol[l].t_net, ly.perm.reshape(-1).cpu().numpy())
+    ozs, _ = O.flow_forward(ol, x[idx].cpu().numpy())
+    for l in range(6):
+        assert rel_err(zs[l][idx].cpu().numpy(), ozs[l]) <= TOL
+
+
+def test_random_flip_state_dict_reload_refreshes_native_tables():
+    """load_state_dict of another random_flip flow (new permutations and
+    weights) after the first native call: the kernels must see the new
+    tables (flows/flows.py:92-99, 110-112)."""
+    a = _make_flow(10, 4, [5, 5], 0.2, 1, random_flip=True)
+    b = _make_flow(10, 4, [5, 5], 0.2, 2, random_flip=True)
+    assert any(not torch.equal(la.perm, lb.perm) for la, lb in zip(a.layers, b.layers))
+    x = _logits(1000, 10, 3)
+    with torch.no_grad():
+        a.transform(x)
+    a.load_state_dict(b.state_dict())
+    with torch.no_grad():
+        z, ld = a.transform(x)
+        xr, _ = a.inverse_transform(z)
+    ol = _oracle_layers(b)
+    for l, ly in enumerate(b.layers):
+        ol[l] = O.OracleLayer(10, ol[l].s_net, ol[l].t_net, ly.perm.reshape(-1).cpu().numpy())
+    ozs, old = O.flow_forward(ol, x.cpu().numpy())
+    assert rel_err(z.cpu().numpy(), ozs[-1]) <= TOL
+    assert rel_err(ld.cpu().numpy(), old) <= TOL
+    assert ((xr - x).abs() / (x.abs() + 1)).max().item() <= TOL
+
+
+def test_data_write_needs_invalidate_and_backward_checks_versions():
+    """Writes through .data bypass version counters: invalidate_native() picks
+    them up.  An in-place weight change between the native forward and its
+    backward raises, as torch autograd does."""
+    f = _make_flow(10, 2, [5, 5], 0.1, 1)
+    x = _logits(256, 10, 1)
+    with torch.no_grad():
+        z0, _ = f.transform(x)
+    f.layers[0].t.layers[0].bias.data.add_(0.5)
+    f.invalidate_native()
+    with torch.no_grad():
+        z1, _ = f.transform(x)
+    ozs, _ = O.flow_forward(_oracle_layers(f), x.cpu().numpy())
+    assert rel_err(z1.cpu().numpy(), ozs[-1]) <= TOL and not torch.equal(z0, z1)
+    z, ld = f.transform(x)           # grad-enabled: native autograd forward
+    with torch.no_grad():
+        f.layers[1].s.layers[0].weight.mul_(2.0)
+    with pytest.raises(RuntimeError, match="modified by an inplace"):
+        (z.sum() + ld.sum()).backward()
+
+
+def test_out_of_range_labels_poison_the_loss_terms():
+    """The reference's probs.gather(1, y) raises on a bad label; the fused
+    kernels turn it into NaN terms and gradients instead of a silent wrong loss."""
+    from cnf_hip import vjp as V
+    f = _make_flow(10, 6, [5, 5], 0.1, 9)
+    stack = f._native_stack()
+    x = _logits(1000, 10, 1)
+    y = torch.randint(0, 10, (1000,), device=DEV, generator=torch.Generator(device=DEV).manual_seed(3))
+    t_ok, _, _ = stack.forward_loss(x, y)
+    assert torch.isfinite(t_ok).all()
+    for bad in (10, -1, 1 << 33):
+        yb = y.clone()
+        yb[17] = bad
+        t, _, _ = stack.forward_loss(x, yb)
+        assert torch.isnan(t[0]) and torch.isnan(t[1]) and torch.isfinite(t[2])
+        tg, g, _ = V.loss_and_grads(stack, x, yb, grad_scale=1e-3)
+        assert torch.isnan(tg[0]) and torch.isnan(g).any()
+
+
+@pytest.mark.parametrize("D,hidden,L,flip", [(10, [5, 5], 6, False), (3, [3, 3], 5, False),
+                                             (10, [5, 5], 3, True), (100, [100, 100], 2, False)])
+def test_fused_predict_matches_reference_formula(D, hidden, L, flip):
+    """cnf_predict (one launch: centring, flow, softmax, prior correction) vs the
+    reference's Calibrator.predict math (calibrators.py:40-44, 350-352) in fp64
+    on the flow's fp32 outputs."""
+    f = _make_flow(D, L, hidden, 0.1, 4, random_flip=flip)
+    stack = f._native_stack()
+    g = torch.Generator(device=DEV).manual_seed(8)
+    x = torch.randn(5000, D, device=DEV, generator=g) * 3 + 1
+    pri = torch.rand(D, generator=torch.Generator().manual_seed(1)).double() + 0.1
+    lp = torch.log(pri / pri.sum())
+    n0 = engine.stats["predict"]
+    probs = stack.predict(x, lp)
+    fused = engine.stats["predict"] == n0 + 1
+    assert fused == (D <= 16 and not flip)   # other shapes compose cnf_forward + torch ops
+    with torch.no_grad():
+        z, _ = f.transform(x - x.mean(dim=1, keepdim=True))
+    p = torch.softmax(z.double(), dim=1).cpu()
+    ref = torch.softmax(torch.log(p + 1e-7) - lp, dim=1).numpy()
+    assert np.max(np.abs(probs.cpu().numpy() - ref)) <= 1e-5

@@ -1,10 +1,12 @@
 #!/bin/bash
-# One GPU-box session: smoke, GPU tests, bench, rocprofv3 kernel-trace summary,
-# and the PMC traffic passes for the bench kernel.  Every GPU step has its own
-# time limit; a fault/abort/timeout ends the script (exit codes other than 0, 1).
-# Usage: bash tools/gpu_check.sh [tag]
+# One GPU-box session: smoke, GPU tests, bench, rocprofv3 kernel-trace summaries
+# of the bench and of every profiled pass, and the PMC passes (traffic and VALU /
+# MFMA issue counters) per pass.  Every GPU step has its own time limit; a
+# fault / abort / timeout ends the script (exit codes other than 0, 1).
+# Usage: bash tools/gpu_check.sh [tag] [quick]
 set -u
-TAG=${1:-r01}
+TAG=${1:-r02}
+QUICK=${2:-}
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -18,10 +20,23 @@ run() {
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
 }
 run smoke 400 python -c "import __graft_entry__ as g; g.smoke()"
-run pytest_gpu 900 python -m pytest tests -m gpu -q
+TAILN=12 run pytest_gpu 900 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread
 TAILN=2 run bench 600 python bench.py
+[ -n "$QUICK" ] && exit 0
 run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python bench.py --steps 100 --no-cpu-baseline --no-variants
-rm -rf gpurun_out/pmc_${TAG}_cfg2
-run pmc 600 bash tools/gpu_pmc.sh $TAG cfg2 "--launches 30" "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SMEM GRBM_GUI_ACTIVE"
-python tools/pmc_traffic.py gpurun_out/pmc_${TAG}_cfg2 gpurun_out/${TAG}_traffic_cfg2.json cfg2 1048576 k_sgpr > /dev/null && cat gpurun_out/${TAG}_traffic_cfg2.json
+# one kernel-trace summary per profiled pass
+for spec in "cfg2 loss" "cfg2 forward" "cfg2 all" "cfg5 forward" "cfg4 forward" "cfg2 train"; do
+  set -- $spec
+  run rocprof_$1_$2 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_$1_$2 -o run --output-format csv -- python tools/prof_target.py --workload $1 --mode $2 --launches 30
+done
+# PMC passes: HBM traffic (separate FETCH / WRITE passes) and issue counters
+VALU="SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM GRBM_GUI_ACTIVE"
+MFMA="SQ_WAVES SQ_INSTS_VALU_MFMA_F32 SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE"
+for spec in "cfg2 loss k_sgpr" "cfg2 all k_sgpr" "cfg2 train k_vjp" "cfg4 forward k_wide"; do
+  set -- $spec
+  rm -rf gpurun_out/pmc_${TAG}_$1_$2_$1
+  CTR="$VALU"; [ "$3" = "k_wide" ] && CTR="$MFMA"; [ "$3" = "k_vjp" ] && CTR="$MFMA"
+  run pmc_$1_$2 600 bash tools/gpu_pmc.sh ${TAG}_$1_$2 $1 "--mode $2 --launches 20" "FETCH_SIZE" "WRITE_SIZE" "$CTR"
+  python tools/pmc_summary.py gpurun_out/pmc_${TAG}_$1_$2_$1 $3 > gpurun_out/${TAG}_pmc_$1_$2.txt 2>&1
+done
 exit 0

@@ -1,5 +1,8 @@
 """Lean profiling target: N launches of one fused pass (no CPU baseline, no
-variants) so rocprofv3 counter passes see only the kernel of interest."""
+variants) so rocprofv3 kernel-trace / counter passes see only the kernels of
+interest.  --mode loss: cnf_forward_loss (the bench step); forward: cnf_forward
+/ cnf_inverse (cfg5); all: every layer's z (the zs list); train: the fused
+calibrator training step cnf_loss_vjp (k_vjp + block-order reductions)."""
 import argparse
 import os
 import sys
@@ -13,16 +16,29 @@ import bench  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--workload", default="cfg2")
 ap.add_argument("--launches", type=int, default=40)
-ap.add_argument("--all", action="store_true")
 ap.add_argument("--batch", type=int, default=0)
-ap.add_argument("--mode", default="loss", choices=["loss", "forward"])
+ap.add_argument("--mode", default="loss", choices=["loss", "forward", "all", "train"])
 a = ap.parse_args()
 w = dict(bench.WORKLOADS[a.workload])
 if a.batch:
     w["B"] = a.batch
-mode = a.mode if (w["D"] <= 16 and not w["inverse"] and not a.all) else "forward"
-r = bench.Runner(w, torch.device("cuda:0"), 1.5e9, all_outputs=a.all, mode=mode)
-for _ in range(a.launches):
-    r.step()
+dev = torch.device("cuda:0")
+if a.mode == "train":
+    from cnf_hip import vjp as V
+    flow = bench.make_flow(w, dev)
+    stack = flow._native_stack()
+    x, y = bench.synthetic_logits(w["B"], w["D"], dev, 4321)
+    for _ in range(a.launches):
+        V.loss_and_grads(stack, x, y, grad_scale=1.0 / w["B"])
+    name = stack.kernel_name()
+else:
+    mode = a.mode
+    if mode == "loss" and (w["D"] > 16 or w["inverse"]):
+        mode = "forward"
+    r = bench.Runner(w, dev, 1.5e9, all_outputs=(mode == "all"),
+                     mode="loss" if mode == "loss" else "forward")
+    for _ in range(a.launches):
+        r.step()
+    name = r.stack.kernel_name()
 torch.cuda.synchronize()
-print("done", r.stack.kernel_name(), w)
+print("done", a.mode, name, w)
