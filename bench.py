@@ -229,13 +229,15 @@ def train_step_rate(dev, B=1 << 20, steps=20):
             "note": "forward + calibrator loss + VJP + gradient reduction; optimizer excluded"}
 
 
-def measured_traffic(workload, B):
+def measured_traffic(workload, B, mode):
     """HBM bytes per launch of the bench kernel from the committed PMC summary
-    (profiles/<round>_traffic_<workload>.json, written by tools/pmc_traffic.py
-    from rocprofv3 FETCH_SIZE / WRITE_SIZE passes, gfx950-corrected), or None."""
+    (profiles/<round>_traffic_<workload>_<mode>.json, written by
+    tools/pmc_traffic.py from rocprofv3 FETCH_SIZE / WRITE_SIZE passes,
+    gfx950-corrected; tools/collect_profiles.sh), newest round first, or None."""
     import glob
     best = None
-    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic_%s.json" % workload))):
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic_%s_%s.json"
+                                           % (workload, mode)))):
         try:
             with open(p) as f:
                 d = json.load(f)
@@ -377,7 +379,7 @@ def main():
         "algo_bytes_per_vec": bytes_vec, "algo_flops_per_vec": flops_vec,
         "rotating_sets": runner.nsets,
     })
-    tr = measured_traffic(args.workload, w["B"])
+    tr = measured_traffic(args.workload, w["B"], mode)
     if tr is not None:
         roof["traffic"] = tr["traffic_bytes_per_launch"]
         roof["traffic_source"] = tr["source"]

@@ -73,9 +73,23 @@ namespace {
 
 using namespace valu;
 
-constexpr int kWaves = 4;   // waves per block
-constexpr int kTR = 128;    // rows per wave tile (lane l: rows 2l, 2l+1)
-constexpr int kWPE = 5;        // register budget: resident waves per SIMD
+constexpr int kWaves = 4;  // waves per block
+
+// Row pairs per lane.  Two pairs (4 rows per lane) let each SGPR weight feed
+// two FMAs (half the scalar-load traffic per row), at 4 waves per SIMD instead
+// of 5; measured on cfg2 it is no faster for the forward pass and 7-19 %
+// slower for the fused loss pass (register pressure), so one pair ships.
+// Every-layer outputs and random_flip stacks always use one pair.
+#ifndef CNF_SGPR_PAIRS
+#define CNF_SGPR_PAIRS 1
+#endif
+template <bool ALL, bool PERM>
+constexpr int pairs_per_lane() { return (ALL || PERM) ? 1 : CNF_SGPR_PAIRS; }
+// register budget (resident waves per SIMD) for a lane of P pairs
+template <int MODE, bool ALL, bool PERM>
+constexpr int waves_per_simd() {
+  return pairs_per_lane<ALL, PERM>() == 2 ? 4 : (PERM ? 4 : 5);
+}
 
 enum Mode { kFwd = 0, kInv = 1, kLoss = 2, kPredict = 3 };
 
@@ -128,80 +142,134 @@ __device__ __forceinline__ f2 fma_clamp(float w, f2 x, f2 acc) {
   return a;
 }
 
-// Issue the loads of one Linear block: plain (compiler-visible) scalar loads,
-// so the compiler's own s_waitcnt guards every read of the destination SGPRs
-// (copies and spills included); the sched_barriers keep the block's
-// s_load_dwordx16s one Linear ahead of their first use.  (An inline-asm
-// load/wait pair let the register allocator copy still-in-flight SGPRs.)
+// Weight-block loads.  Each Linear's block arrives in SGPRs one Linear ahead:
+//   sready()          wait for the block issued one Linear ago -- a
+//                     compiler-visible s_waitcnt lgkmcnt(0), so the compiler
+//                     adds no wait of its own before the block's first use
+//                     (scalar loads return out of order: any later wait
+//                     would be lgkmcnt(0) and would also wait for the block
+//                     issued next);
+//   sissue(next, p)   then issue the next block, before this Linear's FMAs.
+// Plain (compiler-visible) loads: the waitcnt pass guards every read of the
+// destination SGPRs, copies and spills included.  The sched_barriers pin the
+// order wait -> issue -> FMAs, and leave each Linear's neurons one scheduling
+// region.  (An inline-asm load/wait pair let the register allocator copy
+// still-in-flight SGPRs.)
+__device__ __forceinline__ void sready() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0); vmcnt, expcnt untouched (gfx9 encoding)
+  __builtin_amdgcn_sched_barrier(0);
+}
 template <int NC>
 __device__ __forceinline__ void sissue(SW<NC>& r, const float* p) {
   const v16f* q = reinterpret_cast<const v16f*>(__builtin_assume_aligned(p, 64));
-  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int i = 0; i < NC; ++i) r.c[i] = q[i];
   __builtin_amdgcn_sched_barrier(0);
 }
-template <int NC>
-__device__ __forceinline__ void swait(SW<NC>&) {
-  __builtin_amdgcn_sched_barrier(0);
-}
 
-// y[o] = b[o] + sum_k W[o][k] x[k] from an SGPR block of rows
-// [w_o0, b_o, w_o1 .. w_o(NIN-1)] at stride S; RELU: clamped last FMA.
-// after(): issued once the first output neuron is done (the next block's load).
-template <int NIN, int NOUT, int S, bool RELU, int NC, class F>
-__device__ __forceinline__ void slin(const SW<NC>& w, const f2* x, f2* y, F&& after) {
+// Conditioner activations of the lane's P row pairs (pair-major).
+template <int D, int H1, int H2, int P>
+struct Act {
+  f2 c[P][D - D / 2];           // conditioning half (the masked input)
+  f2 h1[P][H1 > 0 ? H1 : 1];
+  f2 h2[P][H2 > 0 ? H2 : 1];
+  f2 t[P][D / 2];               // t-net output, consumed by the s-net's last Linear
+};
+
+// One Linear for the lane's P pairs: neuron o = b[o] + sum_k W[o][k] x(q, k)
+// from an SGPR block of rows [w_o0, b_o, w_o1 .. w_o(NIN-1)] at stride S;
+// RELU: clamped last FMA.  The FMAs run input-major (k outer, neurons inner),
+// so a wave issues NOUT * P independent chains back to back: a lone dependent
+// v_pk_fma_f32 chain issues at half rate (tools/ubench/valu_chain.hip: 9.5
+// vs 5.5 cycles per FMA for one wave, 5.3 vs 4.6 at five waves per SIMD).
+// emit(o, a[P]) consumes neuron o once all are done; before() issues the
+// next block's load once this block has landed.
+template <int NIN, int NOUT, int S, bool RELU, int P, int NC, class X, class E, class F>
+__device__ __forceinline__ void slin(const SW<NC>& w, X&& x, E&& emit, F&& before) {
+  sready();
+  before();
+  f2 a[NOUT][P];
 #pragma unroll
-  for (int o = 0; o < NOUT; ++o) {
-    f2 a;
-    if constexpr (RELU && NIN == 1) a = fma_wb_clamp(w.pair(o * S), x[0]);
-    else a = fma_wb(w.pair(o * S), x[0]);
+  for (int o = 0; o < NOUT; ++o)
 #pragma unroll
-    for (int k = 1; k < NIN; ++k) {
-      if (RELU && k == NIN - 1) a = fma_clamp(w[o * S + 1 + k], x[k], a);
-      else a = fmaT(w[o * S + 1 + k], x[k], a);
+    for (int q = 0; q < P; ++q) {
+      if constexpr (RELU && NIN == 1) a[o][q] = fma_wb_clamp(w.pair(o * S), x(q, 0));
+      else a[o][q] = fma_wb(w.pair(o * S), x(q, 0));
     }
-    y[o] = a;
-    if (o == 0) after();
-  }
+#pragma unroll
+  for (int k = 1; k < NIN; ++k)
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o)
+#pragma unroll
+      for (int q = 0; q < P; ++q) {
+        if (RELU && k == NIN - 1) a[o][q] = fma_clamp(w[o * S + 1 + k], x(q, k), a[o][q]);
+        else a[o][q] = fmaT(w[o * S + 1 + k], x(q, k), a[o][q]);
+      }
+#pragma unroll
+  for (int o = 0; o < NOUT; ++o) emit(o, a[o]);
 }
 
-// Linear IDX of the layer's sequence (net-major: s-net Linears, then t-net);
-// the next block (or the next layer's first, wn) is issued before computing.
-// The two SGPR buffers alternate by the Linear's parity in the layer pair
-// (PAR) -- never a `cur = nxt` copy, which would let the compiler move an
-// in-flight s_load destination before its wait.
-template <class S, int NETS, int IDX, int PAR, bool NEXT>
-__device__ __forceinline__ void run_seq(const f2* c, f2* h1, f2* h2, f2* s, f2* t, SW<S::NC>& A,
-                                        SW<S::NC>& Bf, const float* wl, const float* wn) {
-  if constexpr (IDX < NETS * S::NL) {
-    constexpr int net = IDX / S::NL, i = IDX % S::NL;
+// Float offset of Linear IDX in a layer's block when the t-net runs first
+// (storage keeps the state_dict order: s-net, then t-net).
+template <class S, int NETS, int IDX>
+__device__ __forceinline__ constexpr int lin_at() {
+  return ((NETS == 2 && IDX < S::NL) ? S::NF : 0) + S::off(IDX % S::NL);
+}
+
+// Linear IDX of a layer's sequence: the t-net's Linears, then the s-net's, so
+// the s-net's last Linear applies the affine update neuron by neuron and each
+// s value is consumed as it is produced (upd).  The next block (or the next
+// layer's first, wn) is issued before the FMAs.  The two SGPR buffers
+// alternate by the Linear's parity in the layer pair (PAR) -- never a
+// `cur = nxt` copy, which would let the compiler move an in-flight s_load
+// destination before its wait.
+template <class S, int NETS, int P, int IDX, int PAR, bool NEXT, class AC, class U>
+__device__ __forceinline__ void run_seq(AC& ac, SW<S::NC>& A, SW<S::NC>& Bf, const float* wl,
+                                        const float* wn, U&& upd) {
+  constexpr int NL = S::NL, N = NETS * NL;
+  if constexpr (IDX < N) {
+    constexpr int i = IDX % NL;
+    constexpr bool tnet = IDX < NL, last = i == NL - 1;
     constexpr bool odd = ((IDX + PAR) & 1) != 0;
     SW<S::NC>& cur = odd ? Bf : A;
     SW<S::NC>& nxt = odd ? A : Bf;
-    constexpr bool last = i == S::NL - 1;
-    const f2* in = i == 0 ? c : (i == 1 ? h1 : h2);
-    f2* out = last ? ((NETS == 2 && net == 0) ? s : t) : (i == 0 ? h1 : h2);
-    slin<S::nin(i), S::nout(i), S::stride(i), !last>(cur, in, out, [&]() {
-      if constexpr (IDX + 1 < NETS * S::NL)
-        sissue(nxt, wl + ((IDX + 1) / S::NL) * S::NF + S::off((IDX + 1) % S::NL));
+    auto x = [&](int q, int k) -> f2 {
+      if constexpr (i == 0) return ac.c[q][k];
+      else if constexpr (i == 1) return ac.h1[q][k];
+      else return ac.h2[q][k];
+    };
+    auto emit = [&](int o, const f2* a) {
+#pragma unroll
+      for (int q = 0; q < P; ++q) {
+        if constexpr (!last) {
+          if constexpr (i == 0) ac.h1[q][o] = a[q];
+          else ac.h2[q][o] = a[q];
+        } else if constexpr (tnet && NETS == 2) {
+          ac.t[q][o] = a[q];
+        }
+      }
+      if constexpr (last && (!tnet || NETS == 1)) upd(o, a);
+    };
+    slin<S::nin(i), S::nout(i), S::stride(i), !last, P>(cur, x, emit, [&]() {
+      if constexpr (IDX + 1 < N)
+        sissue(nxt, wl + lin_at<S, NETS, IDX + 1>());
       else if constexpr (NEXT)
-        sissue(nxt, wn);
+        sissue(nxt, wn + lin_at<S, NETS, 0>());
     });
-    swait(nxt);
-    run_seq<S, NETS, IDX + 1, PAR, NEXT>(c, h1, h2, s, t, A, Bf, wl, wn);
+    run_seq<S, NETS, P, IDX + 1, PAR, NEXT>(ac, A, Bf, wl, wn, upd);
   }
 }
 
-// One coupling layer, input in orientation O (O: row held reversed), output in
-// orientation !O -- the flip is a register renaming.  O is also the layer's
-// position in its pair (the second layer's Linears start on buffer parity
-// NETS * NL).  NEXT: prefetch the next layer's first block (wn) -- the pair's
-// first layer does; the pair's last does not, so no SGPR buffer lives across
-// the layer loop's back-edge (a loop-carried buffer makes the allocator rotate
-// it through spill lanes).
-template <int D, int H1, int H2, bool INV, bool O, int NETS, bool PERM, bool NEXT>
-__device__ __forceinline__ void sp_step(f2* v, f2& ld, SW<SP<D, H1, H2>::NC>& A,
+// One coupling layer on the lane's P pairs v[P][D], input in orientation O
+// (O: row held reversed), output in orientation !O -- the flip is a register
+// renaming.  O is also the layer's position in its pair (the second layer's
+// Linears start on buffer parity NETS * NL).  NEXT: prefetch the next layer's
+// first block (wn) -- the pair's first layer does; the pair's last does not,
+// so no SGPR buffer lives across the layer loop's back-edge (a loop-carried
+// buffer makes the allocator rotate it through spill lanes).
+template <int D, int H1, int H2, bool INV, bool O, int NETS, bool PERM, bool NEXT, int P>
+__device__ __forceinline__ void sp_step(f2 (&v)[P][D], f2 (&ld)[P], SW<SP<D, H1, H2>::NC>& A,
                                         SW<SP<D, H1, H2>::NC>& Bf, const float* wl,
                                         const float* wn, bool perm,
                                         const int32_t* __restrict__ q) {
@@ -209,39 +277,51 @@ __device__ __forceinline__ void sp_step(f2* v, f2& ld, SW<SP<D, H1, H2>::NC>& A,
   constexpr int DT = S::DT, DC = S::DC;
   constexpr bool OC = INV ? !O : O;
   if constexpr (INV && PERM) {
-    if (perm) permute<D, O>(v, q);  // flows/flows.py:115-117
-  }
-  f2 c[DC];
+    if (perm) {  // flows/flows.py:115-117
 #pragma unroll
-  for (int k = 0; k < DC; ++k) c[k] = v[R<D, OC>(DT + k)];
-  f2 h1[H1 > 0 ? H1 : 1], h2[H2 > 0 ? H2 : 1], s[DT], t[DT];
-  run_seq<S, NETS, 0, O ? (NETS * S::NL) & 1 : 0, NEXT>(c, h1, h2, s, t, A, Bf, wl, wn);
-#pragma unroll
-  for (int j = 0; j < DT; ++j) {
-    f2& x = v[R<D, OC>(j)];
-    if constexpr (NETS == 1) {  // scale=False: s = 0, exp(0) = 1, log-det += 0
-      x = INV ? x - t[j] : x + t[j];
-    } else if constexpr (!INV) {  // s[j] = log2(e) * s: exp(s) = 2^s[j]
-      x = fmaV(x, exp2T(s[j]), t[j]);
-      ld += s[j];
-    } else {
-      x = (x - t[j]) * exp2T(-s[j]);
-      ld -= s[j];
+      for (int p = 0; p < P; ++p) permute<D, O>(v[p], q);
     }
   }
+  Act<D, H1, H2, P> ac;
+#pragma unroll
+  for (int p = 0; p < P; ++p)
+#pragma unroll
+    for (int k = 0; k < DC; ++k) ac.c[p][k] = v[p][R<D, OC>(DT + k)];
+  // z_j = x_j * exp(s_j) + t_j (inverse: (x_j - t_j) * exp(-s_j)), s_j = log2(e) s
+  // as stored, so exp(s) = 2^s_j and ld accumulates s_j (scaled by ln2 once)
+  auto upd = [&](int j, const f2* a) {
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      f2& x = v[p][R<D, OC>(j)];
+      if constexpr (NETS == 1) {  // scale=False: s = 0, exp(0) = 1, log-det += 0
+        x = INV ? x - a[p] : x + a[p];
+      } else if constexpr (!INV) {
+        x = fmaV(x, exp2T(a[p]), ac.t[p][j]);
+        ld[p] += a[p];
+      } else {
+        x = (x - ac.t[p][j]) * exp2T(-a[p]);
+        ld[p] -= a[p];
+      }
+    }
+  };
+  run_seq<S, NETS, P, 0, O ? (NETS * S::NL) & 1 : 0, NEXT>(ac, A, Bf, wl, wn, upd);
   if constexpr (!INV && PERM) {
-    if (perm) permute<D, O>(v, q);  // flows/flows.py:110-112
+    if (perm) {  // flows/flows.py:110-112
+#pragma unroll
+      for (int p = 0; p < P; ++p) permute<D, O>(v[p], q);
+    }
   }
 }
 
 // ---------------------------------------------------------------------------
-// tile I/O: a lane's two rows are the 2*D contiguous floats at row 2l
+// tile I/O: a lane's 2P rows (pairs p = rows 2P*l + 2p, +1) are the 2*P*D
+// contiguous floats at row 2P*l of the wave's tile
 // ---------------------------------------------------------------------------
-// HBM -> LDS copy of one full wave tile (128*D floats, 16-B aligned) by
+// HBM -> LDS copy of one full wave tile (TR*D floats, 16-B aligned) by
 // LDS-DMA: one global_load_lds_dwordx4 moves 1 KiB, lane-linear.
-template <int D>
+template <int D, int TR>
 __device__ __forceinline__ void wave_dma(float* sm, const float* __restrict__ src, int lane) {
-  constexpr int N4 = 32 * D, NI = (N4 + 63) / 64;
+  constexpr int N4 = TR * D / 4, NI = (N4 + 63) / 64;
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
     if (N4 % 64 == 0 || i * 64 + lane < N4)
@@ -251,31 +331,36 @@ __device__ __forceinline__ void wave_dma(float* sm, const float* __restrict__ sr
   }
 }
 
-// rows 2l, 2l+1 of the LDS tile as packed pairs (one ds_read2_b32 each)
-template <int D>
-__device__ __forceinline__ void read_pairs(const float* sm, int lane, f2* v) {
-  const float* p = sm + 2 * D * lane;
+// the lane's pairs from the LDS tile (one ds_read2_b32 per feature and pair)
+template <int D, int P>
+__device__ __forceinline__ void read_pairs(const float* sm, int lane, f2 (&v)[P][D]) {
+  const float* b = sm + 2 * P * D * lane;
 #pragma unroll
-  for (int k = 0; k < D; ++k) v[k] = f2{p[k], p[D + k]};
+  for (int p = 0; p < P; ++p)
+#pragma unroll
+    for (int k = 0; k < D; ++k) v[p][k] = f2{b[2 * p * D + k], b[(2 * p + 1) * D + k]};
 }
 
-// A lane's 2*D output floats (pairs in logical order) to dst = row 2l:
-// 16-B stores when aligned, else 8-B, else 4-B; `rows` < 2 on the ragged tile.
-template <int D>
-__device__ __forceinline__ void store_pairs(float* __restrict__ dst, const f2* v, int rows,
-                                            int al) {
-  constexpr int NF = 2 * D;
+// The lane's 2*P*D output floats (pairs in logical order) to dst = its first
+// row: 16-B stores when aligned, else 8-B, else 4-B; `rows` < 2P on the ragged
+// tile.
+template <int D, int P>
+__device__ __forceinline__ void store_rows(float* __restrict__ dst, const f2 (&v)[P][D], int rows,
+                                           int al) {
+  constexpr int NF = 2 * P * D;
   float r[NF];
 #pragma unroll
-  for (int k = 0; k < D; ++k) {
-    r[k] = v[k].x;
-    r[D + k] = v[k].y;
-  }
-  if (rows == 2 && NF % 4 == 0 && al >= 16) {
+  for (int p = 0; p < P; ++p)
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      r[2 * p * D + k] = v[p][k].x;
+      r[(2 * p + 1) * D + k] = v[p][k].y;
+    }
+  if (rows == 2 * P && NF % 4 == 0 && al >= 16) {
 #pragma unroll
     for (int q = 0; q < NF / 4; ++q)
       reinterpret_cast<float4*>(dst)[q] = float4{r[4 * q], r[4 * q + 1], r[4 * q + 2], r[4 * q + 3]};
-  } else if (rows == 2 && NF % 2 == 0 && al >= 8) {
+  } else if (rows == 2 * P && NF % 2 == 0 && al >= 8) {
 #pragma unroll
     for (int q = 0; q < NF / 2; ++q) reinterpret_cast<float2*>(dst)[q] = float2{r[2 * q], r[2 * q + 1]};
   } else {
@@ -285,12 +370,20 @@ __device__ __forceinline__ void store_pairs(float* __restrict__ dst, const f2* v
   }
 }
 
-__device__ __forceinline__ void store_ld2(float* __restrict__ dst, f2 ld, int rows, bool al8) {
-  if (rows == 2 && al8) {
-    *reinterpret_cast<float2*>(dst) = float2{ld.x, ld.y};
+template <int P>
+__device__ __forceinline__ void store_lds(float* __restrict__ dst, const f2 (&ld)[P], int rows,
+                                          int al) {
+  if (P == 2 && rows == 4 && al >= 16) {
+    *reinterpret_cast<float4*>(dst) = float4{ld[0].x, ld[0].y, ld[P - 1].x, ld[P - 1].y};
+  } else if (rows == 2 * P && al >= 8) {
+#pragma unroll
+    for (int p = 0; p < P; ++p) reinterpret_cast<float2*>(dst)[p] = float2{ld[p].x, ld[p].y};
   } else {
-    if (rows > 0) dst[0] = ld.x;
-    if (rows > 1) dst[1] = ld.y;
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      if (2 * p < rows) dst[2 * p] = ld[p].x;
+      if (2 * p + 1 < rows) dst[2 * p + 1] = ld[p].y;
+    }
   }
 }
 
@@ -306,38 +399,40 @@ __device__ __forceinline__ void unflip(f2* v) {
   }
 }
 
-// Labels of the lane's rows 2l, 2l+1 (int64 each, one 16-B load when aligned).
-// A label is valid iff 0 <= y < D; an invalid one poisons the loss terms with
-// NaN (the reference's probs.gather raises on it).  rows: valid rows (0..2).
-struct Lab {
-  int y0, y1;
-  bool ok0, ok1;
-};
-template <int D>
-__device__ __forceinline__ Lab load_labels2(const int64_t* __restrict__ y, int rows, bool al16) {
-  Lab r{0, 0, true, true};
-  int lo0 = 0, hi0 = 0, lo1 = 0, hi1 = 0;
+// Labels of the lane's rows (int64 each, 16-B loads when aligned), packed one
+// byte per row into ONE register so they cost no VGPRs across the layer sweep.
+// A label is valid iff 0 <= y < D; an invalid one (byte 0xff) poisons the loss
+// terms with NaN (the reference's probs.gather raises on it).  rows: valid rows.
+template <int D, int P>
+__device__ __forceinline__ uint32_t load_labels(const int64_t* __restrict__ y, int rows,
+                                                bool al16) {
+  uint32_t packed = 0;
   const int32_t* y32 = reinterpret_cast<const int32_t*>(y);
-  if (rows == 2 && al16) {
-    const int4 q = *reinterpret_cast<const int4*>(y32);
-    lo0 = q.x, hi0 = q.y, lo1 = q.z, hi1 = q.w;
-  } else {
-    if (rows > 0) lo0 = y32[0], hi0 = y32[1];
-    if (rows > 1) lo1 = y32[2], hi1 = y32[3];
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    int lo0 = 0, hi0 = 0, lo1 = 0, hi1 = 0;
+    if (rows == 2 * P && al16) {
+      const int4 q = reinterpret_cast<const int4*>(y32)[p];
+      lo0 = q.x, hi0 = q.y, lo1 = q.z, hi1 = q.w;
+    } else {
+      if (2 * p < rows) lo0 = y32[4 * p], hi0 = y32[4 * p + 1];
+      if (2 * p + 1 < rows) lo1 = y32[4 * p + 2], hi1 = y32[4 * p + 3];
+    }
+    const uint32_t b0 = hi0 == 0 && (unsigned)lo0 < (unsigned)D ? (uint32_t)lo0 : 0xffu;
+    const uint32_t b1 = hi1 == 0 && (unsigned)lo1 < (unsigned)D ? (uint32_t)lo1 : 0xffu;
+    packed |= (b0 | (b1 << 8)) << (16 * p);
   }
-  r.ok0 = hi0 == 0 && (unsigned)lo0 < (unsigned)D;
-  r.ok1 = hi1 == 0 && (unsigned)lo1 < (unsigned)D;
-  r.y0 = r.ok0 ? lo0 : 0;
-  r.y1 = r.ok1 ? lo1 : 0;
-  return r;
+  return packed;
 }
 
-// Loss terms of the lane's rows (pairs in logical order):
+// Loss terms of one pair's rows (logical order):
 // CAL: loss = -(log(softmax(z)[y] + 1e-7) + ld)    calibrators.py:288-291
 // CE:  loss = -log_softmax(z)[y] - det * ld         run_experiment3D.py:107
 template <int D>
-__device__ __forceinline__ void pair_loss(const f2* v, f2 ld, const Lab& lab, int rows, int kind,
+__device__ __forceinline__ void pair_loss(const f2* v, f2 ld, uint32_t lab2, int rows, int kind,
                                           float det, float& t0, float& t1, float& t2) {
+  const uint32_t b0 = lab2 & 0xffu, b1 = (lab2 >> 8) & 0xffu;
+  const bool ok[2] = {b0 != 0xffu, b1 != 0xffu};
   constexpr float kL2E = 1.4426950408889634f, kLN2 = 0.6931471805599453f;
   f2 m = v[0];
 #pragma unroll
@@ -352,9 +447,8 @@ __device__ __forceinline__ void pair_loss(const f2* v, f2 ld, const Lab& lab, in
     za[j] = __float_as_uint(v[j].x);
     zb[j] = __float_as_uint(v[j].y);
   }
-  const float zy[2] = {__uint_as_float(sel_tree<D>(za, lab.y0, 0)),
-                       __uint_as_float(sel_tree<D>(zb, lab.y1, 0))};
-  const bool ok[2] = {lab.ok0, lab.ok1};
+  const float zy[2] = {__uint_as_float(sel_tree<D>(za, ok[0] ? (int)b0 : 0, 0)),
+                       __uint_as_float(sel_tree<D>(zb, ok[1] ? (int)b1 : 0, 0))};
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     if (q >= rows) continue;
@@ -443,30 +537,36 @@ struct KArgs {
 // The kernel.  MODE: kFwd / kInv (+ log-det), kLoss (forward + loss terms),
 // kPredict (centre + forward + calibrated probabilities).  ALL: also store
 // every layer's output.  PERM: some layer has a random_flip permutation.
+// A lane carries P row pairs (2P rows), a wave tile 128*P rows.
 template <int D, int H1, int H2, int NETS, int MODE, bool ALL, bool PERM>
-__global__ __launch_bounds__(kWaves * 64, (MODE == kInv && PERM) ? kWPE - 1 : kWPE) void k_sgpr(
+__global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) void k_sgpr(
     const float* __restrict__ W,        // packed-SGPR weight region
     const int32_t* __restrict__ qtab,   // per-layer gather tables (forward or inverse)
     const int32_t* __restrict__ lflag,  // per-layer flags
     const float* __restrict__ lpri,     // log priors [D] (predict)
     KArgs a) {
   using S = SP<D, H1, H2>;
+  constexpr int P = pairs_per_lane<ALL, PERM>();
   constexpr bool INV = MODE == kInv;
   constexpr int LF = NETS * S::NF;  // floats per layer
-  constexpr int TF = kTR * D;       // floats per wave tile
+  constexpr int TR = 128 * P;       // rows per wave tile
+  constexpr int TF = TR * D;        // floats per wave tile
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   float* sm = smem + wv * TF;
   const int64_t B = a.B;
   const int L = a.L;
-  const int nfull = (int)(B / kTR), ntiles = (int)((B + kTR - 1) / kTR);
+  const int nfull = (int)(B / TR), ntiles = (int)((B + TR - 1) / TR);
   const int gw = blockIdx.x * kWaves + wv, nw = gridDim.x * kWaves;
   int left = gw < ntiles ? (ntiles - 1 - gw) / nw + 1 : 0;  // tiles this wave owns
   auto layer_of = [&](int i) { return INV ? L - 1 - i : i; };
-  const int al_out = a.out ? (int)(reinterpret_cast<uintptr_t>(a.out) & 15) : 0;
-  const int al = al_out == 0 ? 16 : ((al_out & 7) == 0 ? 8 : 4);
-  const bool ld8 = a.ld && (reinterpret_cast<uintptr_t>(a.ld) & 7) == 0;
+  auto align_of = [](const void* q) {
+    const int m = (int)(reinterpret_cast<uintptr_t>(q) & 15);
+    return m == 0 ? 16 : ((m & 7) == 0 ? 8 : 4);
+  };
+  const int al = a.out ? align_of(a.out) : 16;
+  const int al_ld = a.ld ? align_of(a.ld) : 16;
   const bool y16 = MODE == kLoss && (reinterpret_cast<uintptr_t>(a.y) & 15) == 0;
   float lp[MODE == kPredict ? D : 1];
   if constexpr (MODE == kPredict) {
@@ -477,16 +577,21 @@ __global__ __launch_bounds__(kWaves * 64, (MODE == kInv && PERM) ? kWPE - 1 : kW
 
   // One tile's compute: rows in v (orientation 0) -> outputs in v (logical
   // order), log-det in ld; every-layer stores on the way (rows valid: nr).
-  auto compute = [&](f2* v, f2& ld, int64_t row0, int nr) {
-    if constexpr (MODE == kPredict) centre<D>(v);
-    ld = splat(0.f, f2{});
+  auto compute = [&](f2 (&v)[P][D], f2 (&ld)[P], int64_t row0, int nr) {
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      if constexpr (MODE == kPredict) centre<D>(v[p]);
+      ld[p] = splat(0.f, f2{});
+    }
     auto st_all = [&](int i, auto O_) {
       if constexpr (ALL) {
         constexpr bool O = decltype(O_)::value;
-        f2 o[D];
+        f2 o[P][D];
 #pragma unroll
-        for (int j = 0; j < D; ++j) o[j] = v[R<D, O>(j)];
-        store_pairs<D>(a.all + ((int64_t)i * B + row0 + 2 * lane) * D, o, nr, al);
+        for (int p = 0; p < P; ++p)
+#pragma unroll
+          for (int j = 0; j < D; ++j) o[p][j] = v[p][R<D, O>(j)];
+        store_rows<D, P>(a.all + ((int64_t)i * B + row0 + 2 * P * lane) * D, o, nr, 16);
       }
     };
     int i = 0;
@@ -497,12 +602,12 @@ __global__ __launch_bounds__(kWaves * 64, (MODE == kInv && PERM) ? kWPE - 1 : kW
       const float* wa = W + (int64_t)la * LF;
       const float* wb = W + (int64_t)lb * LF;
       SW<S::NC> cur, alt;
-      sissue(cur, wa);
-      swait(cur);
-      sp_step<D, H1, H2, INV, false, NETS, PERM, true>(v, ld, cur, alt, wa, wb, pa, qtab + la * D);
+      sissue(cur, wa + lin_at<S, NETS, 0>());
+      sp_step<D, H1, H2, INV, false, NETS, PERM, true, P>(v, ld, cur, alt, wa, wb, pa,
+                                                          qtab + la * D);
       st_all(i, std::true_type{});
-      sp_step<D, H1, H2, INV, true, NETS, PERM, false>(v, ld, cur, alt, wb, nullptr, pb,
-                                                       qtab + lb * D);
+      sp_step<D, H1, H2, INV, true, NETS, PERM, false, P>(v, ld, cur, alt, wb, nullptr, pb,
+                                                          qtab + lb * D);
       st_all(i + 1, std::false_type{});
     }
     if (i < L) {
@@ -510,15 +615,26 @@ __global__ __launch_bounds__(kWaves * 64, (MODE == kInv && PERM) ? kWPE - 1 : kW
       const bool pa = PERM && (lflag[la] & kFlagPerm);
       const float* wa = W + (int64_t)la * LF;
       SW<S::NC> cur, alt;
-      sissue(cur, wa);
-      swait(cur);
-      sp_step<D, H1, H2, INV, false, NETS, PERM, false>(v, ld, cur, alt, wa, nullptr, pa,
-                                                        qtab + la * D);
+      sissue(cur, wa + lin_at<S, NETS, 0>());
+      sp_step<D, H1, H2, INV, false, NETS, PERM, false, P>(v, ld, cur, alt, wa, nullptr, pa,
+                                                           qtab + la * D);
       st_all(i, std::true_type{});
-      unflip<D>(v);
+#pragma unroll
+      for (int p = 0; p < P; ++p) unflip<D>(v[p]);
     }
-    if constexpr (NETS == 2) ld = ld * splat(0.69314718055994531f, f2{});  // ln2 * sum(s')
-    if constexpr (MODE == kPredict) pair_predict<D>(v, lp);
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      if constexpr (NETS == 2) ld[p] = ld[p] * splat(0.69314718055994531f, f2{});  // ln2 sum(s')
+      if constexpr (MODE == kPredict) pair_predict<D>(v[p], lp);
+    }
+  };
+  auto loss = [&](const f2 (&v)[P][D], const f2 (&ld)[P], uint32_t lab, int nr) {
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      const int r = nr - 2 * p;
+      pair_loss<D>(v[p], ld[p], lab >> (16 * p), r < 0 ? 0 : (r > 2 ? 2 : r), a.kind, a.det, lt0,
+                   lt1, lt2);
+    }
   };
 
   // -------- full tiles: LDS-DMA in, deferred 16-B stores out --------
@@ -530,9 +646,9 @@ __global__ __launch_bounds__(kWaves * 64, (MODE == kInv && PERM) ? kWPE - 1 : kW
   int ntr = 0;
 #endif
   int t = gw;
-  if (t < nfull) wave_dma<D>(sm, a.in + (int64_t)t * TF, lane);
-  f2 pz[D], pld = splat(0.f, f2{});
-  int64_t prow = -1;  // row 2l of the pending (not yet stored) outputs
+  if (t < nfull) wave_dma<D, TR>(sm, a.in + (int64_t)t * TF, lane);
+  f2 pz[P][D], pld[P];
+  int64_t prow = -1;  // first row of the lane's pending (not yet stored) outputs
   for (; t < nfull; t += nw) {
     --left;  // tiles after this one
     if (left >= 3) __builtin_amdgcn_s_setprio(3);
@@ -540,55 +656,61 @@ __global__ __launch_bounds__(kWaves * 64, (MODE == kInv && PERM) ? kWPE - 1 : kW
     else if (left == 1) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA has landed
-    f2 v[D];
-    read_pairs<D>(sm, lane, v);
+    f2 v[P][D];
+    read_pairs<D, P>(sm, lane, v);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // rows are in registers
 #ifdef CNF_SGPR_TRACE
     if (ntr < 2) CNF_TR(1 + 2 * ntr);
 #endif
-    const int64_t row0 = (int64_t)t * kTR;
+    const int64_t row0 = (int64_t)t * TR;
     if (prow >= 0) {  // the previous tile's outputs, issued after this tile's reads
-      if (a.out) store_pairs<D>(a.out + prow * D, pz, 2, al);
-      if (a.ld) store_ld2(a.ld + prow, pld, 2, ld8);
+      if (a.out) store_rows<D, P>(a.out + prow * D, pz, 2 * P, al);
+      if (a.ld) store_lds<P>(a.ld + prow, pld, 2 * P, al_ld);
     }
-    if (t + nw < nfull) wave_dma<D>(sm, a.in + (int64_t)(t + nw) * TF, lane);
-    Lab lab{};
-    if constexpr (MODE == kLoss) lab = load_labels2<D>(a.y + row0 + 2 * lane, 2, y16);
-    f2 ld;
-    compute(v, ld, row0, 2);
-    if constexpr (MODE == kLoss) pair_loss<D>(v, ld, lab, 2, a.kind, a.det, lt0, lt1, lt2);
+    if (t + nw < nfull) wave_dma<D, TR>(sm, a.in + (int64_t)(t + nw) * TF, lane);
+    uint32_t lab = 0;
+    if constexpr (MODE == kLoss) lab = load_labels<D, P>(a.y + row0 + 2 * P * lane, 2 * P, y16);
+    f2 ld[P];
+    compute(v, ld, row0, 2 * P);
+    if constexpr (MODE == kLoss) loss(v, ld, lab, 2 * P);
 #ifdef CNF_SGPR_TRACE
     if (ntr < 2) CNF_TR(2 + 2 * ntr);
     CNF_TR(5);
     ++ntr;
 #endif
 #pragma unroll
-    for (int k = 0; k < D; ++k) pz[k] = v[k];
-    pld = ld;
-    prow = row0 + 2 * lane;
+    for (int p = 0; p < P; ++p) {
+#pragma unroll
+      for (int k = 0; k < D; ++k) pz[p][k] = v[p][k];
+      pld[p] = ld[p];
+    }
+    prow = row0 + 2 * P * lane;
   }
   if (prow >= 0) {
-    if (a.out) store_pairs<D>(a.out + prow * D, pz, 2, al);
-    if (a.ld) store_ld2(a.ld + prow, pld, 2, ld8);
+    if (a.out) store_rows<D, P>(a.out + prow * D, pz, 2 * P, al);
+    if (a.ld) store_lds<P>(a.ld + prow, pld, 2 * P, al_ld);
   }
-  // -------- the ragged last tile (B % 128 rows): plain loads, masked stores --------
+  // -------- the ragged last tile (B % TR rows): plain loads, masked stores --------
   if (t == nfull && nfull < ntiles) {
-    const int64_t row0 = (int64_t)t * kTR;
-    const int64_t r = row0 + 2 * lane;
-    const int nr = r >= B ? 0 : (r + 1 >= B ? 1 : 2);
-    f2 v[D];
+    const int64_t row0 = (int64_t)t * TR;
+    const int64_t r = row0 + 2 * P * lane;
+    const int64_t left_rows = B - r;
+    const int nr = left_rows <= 0 ? 0 : (left_rows >= 2 * P ? 2 * P : (int)left_rows);
+    f2 v[P][D];
 #pragma unroll
-    for (int k = 0; k < D; ++k) {
-      v[k].x = nr > 0 ? a.in[r * D + k] : 0.f;
-      v[k].y = nr > 1 ? a.in[(r + 1) * D + k] : 0.f;
-    }
-    Lab lab{};
-    if constexpr (MODE == kLoss) lab = load_labels2<D>(a.y + r, nr, false);
-    f2 ld;
+    for (int p = 0; p < P; ++p)
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        v[p][k].x = 2 * p < nr ? a.in[(r + 2 * p) * D + k] : 0.f;
+        v[p][k].y = 2 * p + 1 < nr ? a.in[(r + 2 * p + 1) * D + k] : 0.f;
+      }
+    uint32_t lab = 0;
+    if constexpr (MODE == kLoss) lab = load_labels<D, P>(a.y + r, nr, false);
+    f2 ld[P];
     compute(v, ld, row0, nr);
-    if constexpr (MODE == kLoss) pair_loss<D>(v, ld, lab, nr, a.kind, a.det, lt0, lt1, lt2);
-    if (a.out) store_pairs<D>(a.out + r * D, v, nr, 4);
-    if (a.ld) store_ld2(a.ld + r, ld, nr, false);
+    if constexpr (MODE == kLoss) loss(v, ld, lab, nr);
+    if (a.out) store_rows<D, P>(a.out + r * D, v, nr, 4);
+    if (a.ld) store_lds<P>(a.ld + r, ld, nr, 4);
   }
   CNF_TR(6);
   if constexpr (MODE == kLoss) block_sum3<kWaves * 64>(lt0, lt1, lt2, smem, a.part);
@@ -596,23 +718,31 @@ __global__ __launch_bounds__(kWaves * 64, (MODE == kInv && PERM) ? kWPE - 1 : kW
 
 using KFn = void (*)(const float*, const int32_t*, const int32_t*, const float*, KArgs);
 
+// one instantiation and the rows of its wave tile
+struct KV {
+  KFn fn;
+  int tr;
+};
+
 // variants without permutation: fwd, inv, loss, predict, fwd+all, inv+all;
 // with a random_flip permutation: fwd, inv, fwd+all, inv+all
 enum Var { vFwd, vInv, vLoss, vPredict, vFwdAll, vInvAll, kNVar };
 
 struct SEntry {
   int D, H1, H2;
-  KFn fn[2][kNVar];  // [nets - 1][variant]
-  KFn pfn[2][4];     // [nets - 1][fwd, inv, fwd+all, inv+all] with permutation
+  KV fn[2][kNVar];  // [nets - 1][variant]
+  KV pfn[2][4];     // [nets - 1][fwd, inv, fwd+all, inv+all] with permutation
 };
 
+#define CNF_K(D, H1, H2, N, M, A, P) \
+  {k_sgpr<D, H1, H2, N, M, A, P>, 128 * pairs_per_lane<A, P>()}
 #define CNF_SV(D, H1, H2, N)                                                                  \
-  {k_sgpr<D, H1, H2, N, kFwd, false, false>, k_sgpr<D, H1, H2, N, kInv, false, false>,         \
-   k_sgpr<D, H1, H2, N, kLoss, false, false>, k_sgpr<D, H1, H2, N, kPredict, false, false>,    \
-   k_sgpr<D, H1, H2, N, kFwd, true, false>, k_sgpr<D, H1, H2, N, kInv, true, false>}
+  {CNF_K(D, H1, H2, N, kFwd, false, false), CNF_K(D, H1, H2, N, kInv, false, false),           \
+   CNF_K(D, H1, H2, N, kLoss, false, false), CNF_K(D, H1, H2, N, kPredict, false, false),      \
+   CNF_K(D, H1, H2, N, kFwd, true, false), CNF_K(D, H1, H2, N, kInv, true, false)}
 #define CNF_SP(D, H1, H2, N)                                                                  \
-  {k_sgpr<D, H1, H2, N, kFwd, false, true>, k_sgpr<D, H1, H2, N, kInv, false, true>,           \
-   k_sgpr<D, H1, H2, N, kFwd, true, true>, k_sgpr<D, H1, H2, N, kInv, true, true>}
+  {CNF_K(D, H1, H2, N, kFwd, false, true), CNF_K(D, H1, H2, N, kInv, false, true),             \
+   CNF_K(D, H1, H2, N, kFwd, true, true), CNF_K(D, H1, H2, N, kInv, true, true)}
 #define CNF_SGPR(D, H1, H2) \
   {D, H1, H2, {CNF_SV(D, H1, H2, 1), CNF_SV(D, H1, H2, 2)}, {CNF_SP(D, H1, H2, 1), CNF_SP(D, H1, H2, 2)}}
 
@@ -636,39 +766,41 @@ const SEntry* find(const Shape& s) {
   return nullptr;
 }
 
-size_t lds_bytes(const Shape& s) { return (size_t)kWaves * kTR * s.D * 4; }
+size_t lds_bytes(const Shape& s, const KV& k) { return (size_t)kWaves * k.tr * s.D * 4; }
 
-int resident_blocks(KFn fn, size_t lds) {
+int resident_blocks(const KV& k, size_t lds) {
   static std::mutex mu;
   static std::unordered_map<const void*, int> cache;
   std::lock_guard<std::mutex> g(mu);
-  auto it = cache.find((const void*)fn);
+  auto it = cache.find((const void*)k.fn);
   if (it != cache.end()) return it->second;
   int n = 0, dev = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kWaves * 64, lds) != hipSuccess || n < 1)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k.fn, kWaves * 64, lds) != hipSuccess ||
+      n < 1)
     n = 1;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
       cus < 1)
     cus = 256;
-  cache[(const void*)fn] = n * cus;
+  cache[(const void*)k.fn] = n * cus;
   return n * cus;
 }
 
-KFn pick(const SEntry* e, const Shape& s, int mode, bool all) {
+const KV* pick(const SEntry* e, const Shape& s, int mode, bool all) {
   const int n = s.scale ? 1 : 0;
   if (s.any_perm) {
     if (mode == kLoss || mode == kPredict) return nullptr;  // k_valu handles these
-    return e->pfn[n][(mode == kInv ? 1 : 0) + (all ? 2 : 0)];
+    return &e->pfn[n][(mode == kInv ? 1 : 0) + (all ? 2 : 0)];
   }
-  if (all) return e->fn[n][mode == kInv ? vInvAll : vFwdAll];
-  return e->fn[n][mode];
+  if (all) return &e->fn[n][mode == kInv ? vInvAll : vFwdAll];
+  return &e->fn[n][mode];
 }
 
-int64_t grid_for(KFn fn, const Shape& s, int64_t B) {
-  const int64_t ntiles = (B + kTR - 1) / kTR;
+// persistent grid: every wave of a resident block walks tiles
+int64_t grid_for(const KV& k, const Shape& s, int64_t B) {
+  const int64_t ntiles = (B + k.tr - 1) / k.tr;
   const int64_t want = (ntiles + kWaves - 1) / kWaves;
-  const int64_t cap = resident_blocks(fn, lds_bytes(s));
+  const int64_t cap = resident_blocks(k, lds_bytes(s, k));
   return want < cap ? want : cap;
 }
 
@@ -687,8 +819,8 @@ bool sgpr_enabled(const Shape& s) {
 
 int64_t sgpr_blocks(const Shape& s, int64_t B) {
   const SEntry* e = find(s);
-  KFn fn = e ? pick(e, s, kLoss, false) : nullptr;
-  return fn ? grid_for(fn, s, B) : 0;
+  const KV* k = e ? pick(e, s, kLoss, false) : nullptr;
+  return k ? grid_for(*k, s, B) : 0;
 }
 
 int sgpr_run(const Shape& s, const void* prepared, const float* in, float* out, float* ld,
@@ -697,11 +829,11 @@ int sgpr_run(const Shape& s, const void* prepared, const float* in, float* out, 
   const SEntry* e = find(s);
   if (!e || !sgpr_enabled(s)) return CNF_ERR_UNSUPPORTED;
   if (B == 0) return CNF_OK;
-  if ((B + kTR - 1) / kTR > 0x7fffffffLL) return CNF_ERR_UNSUPPORTED;
+  if (B / 128 > 0x7fffffffLL) return CNF_ERR_UNSUPPORTED;
   if (!io_ok(in, 16) || !io_ok(out, 4) || !io_ok(all, 16) || !io_ok(ld, 4)) return CNF_ERR_UNSUPPORTED;
   const int mode = log_priors ? kPredict : (loss_ws ? kLoss : (inverse ? kInv : kFwd));
-  KFn fn = pick(e, s, mode, all != nullptr);
-  if (!fn) return CNF_ERR_UNSUPPORTED;
+  const KV* k = pick(e, s, mode, all != nullptr);
+  if (!k) return CNF_ERR_UNSUPPORTED;
   const char* base = static_cast<const char*>(prepared);
   const int32_t* fwd_q = reinterpret_cast<const int32_t*>(base);
   const int32_t* inv_q = fwd_q + s.L * s.D;
@@ -718,8 +850,8 @@ int sgpr_run(const Shape& s, const void* prepared, const float* in, float* out, 
   a.L = s.L;
   a.kind = kind;
   a.det = det;
-  const int64_t nblk = grid_for(fn, s, B);
-  hipLaunchKernelGGL(fn, dim3((unsigned)nblk), dim3(kWaves * 64), lds_bytes(s), st, W,
+  const int64_t nblk = grid_for(*k, s, B);
+  hipLaunchKernelGGL(k->fn, dim3((unsigned)nblk), dim3(kWaves * 64), lds_bytes(s, *k), st, W,
                      inverse ? inv_q : fwd_q, flags, log_priors, a);
   if (mode == kLoss) reduce_partials(loss_ws + 4, (int)nblk, 4, 0, nullptr, loss_terms, st);
   hipError_t err = hipGetLastError();

@@ -1,0 +1,22 @@
+#!/bin/bash
+# Copy one gpu_check.sh session's summaries from gpurun_out/ into profiles/
+# (tracked): kernel-trace stats per pass, PMC medians, HBM traffic per launch,
+# and the bench line.  usage: tools/collect_profiles.sh TAG
+set -eu
+TAG=$1
+cd "$(dirname "$0")/.."
+mkdir -p profiles
+cp gpurun_out/prof_${TAG}/run_kernel_stats.csv profiles/${TAG}_bench_kernel_stats.csv
+for d in gpurun_out/prof_${TAG}_*; do
+  n=${d#gpurun_out/prof_${TAG}_}
+  [ -f $d/run_kernel_stats.csv ] && cp $d/run_kernel_stats.csv profiles/${TAG}_${n}_kernel_stats.csv
+done
+for spec in "cfg2 loss k_sgpr 1048576" "cfg2 all k_sgpr 1048576" "cfg2 train k_vjp 1048576" "cfg4 forward k_wide 262144"; do
+  set -- $spec
+  dir=gpurun_out/pmc_${TAG}_$1_$2_$1
+  [ -d $dir ] || continue
+  python tools/pmc_summary.py $dir $3 > profiles/${TAG}_pmc_$1_$2.txt
+  python tools/pmc_traffic.py $dir profiles/${TAG}_traffic_$1_$2.json $1 $4 $3 > /dev/null
+done
+grep '^{"metric"' gpurun_out/bench.log | tail -1 >> profiles/${TAG}_bench.jsonl
+ls profiles/ | grep "^${TAG}_"

@@ -19,7 +19,8 @@ from cnf_hip import _lib  # noqa: E402
 mode = sys.argv[1] if len(sys.argv) > 1 else "loss"
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 20
 w = dict(bench.WORKLOADS["cfg2"], B=B)
-r = bench.Runner(w, torch.device("cuda:0"), 0.5e9, mode=mode)
+r = bench.Runner(w, torch.device("cuda:0"), 0.5e9, all_outputs=(mode == "all"),
+                 mode="loss" if mode == "loss" else "forward")
 for _ in range(20):
     r.step()
 torch.cuda.synchronize()
