@@ -115,6 +115,33 @@ def lib():
     return _lib
 
 
+TORCH_LIB_PATH = os.environ.get("CNF_TORCH_LIB", os.path.join(_HERE, "libcnf_torch.so"))
+_ops = None
+_ops_tried = False
+
+
+def torch_ops():
+    """torch.ops.cnf (the TORCH_LIBRARY operators of csrc/cnf_torch_ops.cpp over
+    the same C ABI), or None when libcnf_torch.so was not built.  Loaded after
+    libcnf_hip.so so both resolve to the one in-tree copy."""
+    global _ops, _ops_tried
+    if not _ops_tried:
+        with _lock:
+            if not _ops_tried:
+                lib()
+                if os.path.exists(TORCH_LIB_PATH):
+                    torch.ops.load_library(TORCH_LIB_PATH)
+                    _ops = torch.ops.cnf
+                _ops_tried = True
+    return _ops
+
+
+def desc_list(d):
+    """cnf_desc as the int[] the torch operators take."""
+    return [d.dim, d.n_layers, d.n_hidden] + [d.hidden[i] for i in range(MAX_HIDDEN)] + \
+        [d.scale, d.shift, d.strict_nan, d.options]
+
+
 def check(fn, status):
     if status != 0:
         l = lib()

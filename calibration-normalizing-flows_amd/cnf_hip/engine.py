@@ -21,8 +21,18 @@ import torch
 
 from . import _lib
 
-# counts of native launches (tests assert the HIP path really ran)
-stats = {"forward": 0, "inverse": 0, "prepare": 0, "vjp": 0, "loss_vjp": 0, "predict": 0}
+# counts of native launches (tests assert the HIP path really ran); "torch_ops"
+# counts the launches that went through the torch.library operators
+stats = {"forward": 0, "inverse": 0, "prepare": 0, "vjp": 0, "loss_vjp": 0, "predict": 0,
+         "torch_ops": 0}
+
+# Dispatch through torch.ops.cnf (C++ operators, autograd in C++) when
+# libcnf_torch.so is built; False: the ctypes calls of the same C ABI.
+USE_TORCH_OPS = True
+
+
+def _ops():
+    return _lib.torch_ops() if USE_TORCH_OPS else None
 
 
 def _ptr(t):
@@ -55,6 +65,10 @@ class CouplingStack:
         self.L = len(layers)
         self._perm_key = None
         self._perms = None
+        # the Parameter objects are fixed for the stack's life (load_state_dict
+        # and .to() update them in place); nn.Module attribute lookups cost
+        # ~4 us each, so the list is gathered once
+        self._params = self._gather_params()
         self._refresh_desc()
         self._cache = {}
         self._loss_ws = {}
@@ -80,6 +94,7 @@ class CouplingStack:
             self._perms = None
         self.desc = _lib.make_desc(self.dim, self.L, self.hidden, self.scale, self.shift,
                                    self.strict_nan, self._perms, self.options)
+        self.desc_ints = _lib.desc_list(self.desc)
 
     def invalidate(self):
         """Forget every prepared blob (after writes the version counters do
@@ -98,6 +113,9 @@ class CouplingStack:
 
     def param_tensors(self):
         """ABI order (include/cnf.h cnf_param_tensor_count)."""
+        return self._params
+
+    def _gather_params(self):
         out = []
         for ly in self.layers:
             for net, on in ((ly.s, self.scale), (ly.t, self.shift)):
@@ -115,16 +133,14 @@ class CouplingStack:
 
     def state_key(self):
         """Identity of everything the prepared blob encodes."""
-        return (tuple((p.data_ptr(), p._version) for p in self.param_tensors()),
-                self._perm_state())
+        return (tuple([(p.data_ptr(), p._version) for p in self._params]), self._perm_state())
+
+    def requires_grad(self):
+        return any([p.requires_grad for p in self._params])
 
     def prepared(self, device):
         """Device blob for this stack, rebuilt only when a parameter or a
         permutation changed (storage or in-place version counter)."""
-        ps = self.param_tensors()
-        for p in ps:
-            if p.device != device or p.dtype != torch.float32:
-                raise TypeError("native coupling path needs fp32 parameters on %s" % device)
         if self._perm_state() != self._perm_key:
             self._refresh_desc()
             self._cache.clear()
@@ -132,6 +148,10 @@ class CouplingStack:
         ent = self._cache.get(device)
         if ent is not None and ent[0] == key:
             return ent[1]
+        ps = self._params
+        for p in ps:
+            if p.device != device or p.dtype != torch.float32:
+                raise TypeError("native coupling path needs fp32 parameters on %s" % device)
         lib = _lib.lib()
         nbytes = ctypes.c_size_t()
         _lib.check("cnf_prepared_bytes", lib.cnf_prepared_bytes(ctypes.byref(self.desc),
@@ -164,6 +184,14 @@ class CouplingStack:
         dev = x.device
         if blob is None:
             blob = self.prepared(dev)
+        ops = _ops()
+        if ops is not None:
+            out, ld = ops.forward(x, blob, self.desc_ints, self._perms, inverse, want_all)
+            stats["inverse" if inverse else "forward"] += 1
+            stats["torch_ops"] += 1
+            if want_all:
+                return (out[-1] if want_final else None), ld, out
+            return out, ld, None
         ld = torch.empty(B, dtype=torch.float32, device=dev)
         allt = torch.empty(self.L, B, self.dim, dtype=torch.float32, device=dev) \
             if want_all else None
@@ -240,8 +268,16 @@ class CouplingStack:
 
     # -------------------------------------------------------------- autograd
     def forward_autograd(self, x, want_all):
-        """Forward with gradients w.r.t. x and every parameter (cnf_vjp)."""
+        """Forward with gradients w.r.t. x and every parameter (cnf_vjp): the
+        cnf::flow operator (autograd kernel in C++) or the Python Function."""
         ps = self.param_tensors()
+        ops = _ops()
+        if ops is not None:
+            x = self._check_input(x)
+            blob = self.prepared(x.device)
+            stats["forward"] += 1
+            stats["torch_ops"] += 1
+            return ops.flow(x, blob, self.desc_ints, self._perms, want_all, ps)
         return _StackFn.apply(self, want_all, x, *ps)
 
 

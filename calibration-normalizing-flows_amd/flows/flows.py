@@ -131,7 +131,7 @@ class Flow(nn.Module):
         from cnf_hip._lib import UnsupportedShape
         stack = self._native_stack()
         try:
-            if _needs_grad(x, self):
+            if torch.is_grad_enabled() and (x.requires_grad or stack.requires_grad()):
                 if inverse:
                     # no native reverse mode of the inverse: the reference's ops
                     _not_native("autograd through the inverse (Flow.backward)")

@@ -102,3 +102,18 @@ def test_forward_argument_validation_without_gpu():
     # B == 0 is a no-op
     assert lib.cnf_forward(ctypes.byref(d), P(0), P(0), P(0), P(0), P(0),
                            ctypes.c_int64(0), P(0)) == 0
+
+
+def test_torch_library_operators_register():
+    """csrc/cnf_torch_ops.cpp registers the cnf::* operators (TORCH_LIBRARY)
+    over the same C ABI; loading needs no GPU."""
+    from cnf_hip import _lib
+    ops = _lib.torch_ops()
+    assert ops is not None, "libcnf_torch.so was not built"
+    names = {"forward", "flow", "forward_loss", "loss_and_grads", "vjp", "predict"}
+    for n in names:
+        assert hasattr(ops, n), n
+    sch = str(torch.ops.cnf.flow.default._schema)
+    assert "Tensor[] params" in sch and "int[] desc" in sch
+    d = _lib.make_desc(10, 6, [5, 5])
+    assert _lib.desc_list(d) == [10, 6, 2, 5, 5, 0, 0, 0, 0, 0, 0, 1, 1, 0, 0]

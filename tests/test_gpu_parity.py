@@ -397,3 +397,49 @@ def test_fused_predict_matches_reference_formula(D, hidden, L, flip):
     p = torch.softmax(z.double(), dim=1).cpu()
     ref = torch.softmax(torch.log(p + 1e-7) - lp, dim=1).numpy()
     assert np.max(np.abs(probs.cpu().numpy() - ref)) <= 1e-5
+
+
+@pytest.mark.parametrize("name", ["g2_nvp_d10_n02", "g6_d10_randflip", "g3_nvp_d100_n003",
+                                  "g1_nice_d3_n02"])
+@pytest.mark.parametrize("via_ops", [True, False])
+def test_torch_ops_and_ctypes_boundaries_agree_with_fixture(name, via_ops, monkeypatch):
+    """Both host boundaries -- the cnf::* torch.library operators (C++) and the
+    ctypes calls -- reach the same kernels and match the reference fixture."""
+    monkeypatch.setattr(engine, "USE_TORCH_OPS", via_ops)
+    meta, state, d = load(name)
+    flow = build_flow(meta, state, DEV)
+    x = torch.from_numpy(d["x"]).to(DEV)
+    n0 = engine.stats["torch_ops"]
+    with torch.no_grad():
+        zs, ld = flow(x)
+        z, _ = flow.transform(x)
+    assert (engine.stats["torch_ops"] - n0 == 2) == via_ops
+    assert rel_err(torch.stack(zs).cpu().numpy(), d["zs"]) <= TOL
+    assert rel_err(ld.cpu().numpy(), d["ld"]) <= TOL
+    assert rel_err(z.cpu().numpy(), d["zs"][-1]) <= TOL
+
+
+def test_torch_ops_autograd_matches_reference_gradients():
+    """cnf::flow's C++ autograd kernel (backward = cnf_vjp) against the
+    reference's own autograd gradients (g5 fixture, calibrators.py:288-291)."""
+    from cnf_hip import _lib
+    assert _lib.torch_ops() is not None
+    meta, state, d = load("g5_grads_d10")
+    flow = build_flow(meta, state, DEV)
+    x = torch.from_numpy(d["x"]).to(DEV)
+    y = torch.from_numpy(d["y"]).to(DEV)
+    n0 = engine.stats["torch_ops"]
+    zs, ld = flow(x)
+    assert engine.stats["torch_ops"] == n0 + 1
+    probs = torch.softmax(zs[-1], dim=1)
+    ce = torch.log(probs.gather(1, y.view(-1, 1)) + 1e-7)
+    loss = -torch.mean(ce.squeeze() + ld)
+    flow.zero_grad()
+    loss.backward()
+    worst = 0.0
+    for k, p in flow.named_parameters():
+        if p.requires_grad:
+            ref = d["gcal:" + k]
+            worst = max(worst, float(np.max(np.abs(p.grad.cpu().numpy() - ref))) /
+                        (float(np.max(np.abs(ref))) + 1e-3))
+    assert worst <= 1e-4, worst
