@@ -42,6 +42,7 @@ struct Shape {
   int64_t sp_lin_off[kMaxLin] = {};
   int64_t sp_net_floats = 0;
   int64_t sp_region = 0;  // float offset of the region in the weights region
+  int64_t vp_region = 0;  // the same layout with plain (unscaled) weights: reverse mode
   // tile (MFMA) layout
   int NO = 0;                        // last-linear outputs computed: DT (fast) or D (strict)
   int lin_nin[kMaxLin] = {}, lin_nout[kMaxLin] = {}, lin_inoff[kMaxLin] = {};
@@ -99,6 +100,7 @@ int wide_run(const Shape& s, const void* prepared, const float* in, float* out, 
              int64_t B, bool inverse, hipStream_t st);
 
 int vjp_workspace(const Shape& s, int64_t B, size_t* bytes);
+bool vjp2_ok(const Shape& s);  // the packed-pair SGPR reverse-mode kernel serves this shape
 // kind < 0: generic VJP from gz / gz_all / gld;  kind = CNF_LOSS_*: fused loss
 int vjp_run(const Shape& s, const void* prepared, const float* x, const int64_t* y,
             const float* gz, const float* gz_all, const float* gld, int kind, float det,

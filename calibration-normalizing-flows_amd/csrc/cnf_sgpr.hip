@@ -52,6 +52,7 @@
 #include "cnf_internal.h"
 #include "cnf_valu_common.h"
 #include "cnf_valu_io.h"
+#include "cnf_sgpr_common.h"
 
 #ifdef CNF_SGPR_TRACE
 // Diagnostic build only (make trace, never shipped): per-wave s_memrealtime
@@ -92,81 +93,6 @@ constexpr int waves_per_simd() {
 }
 
 enum Mode { kFwd = 0, kInv = 1, kLoss = 2, kPredict = 3 };
-
-// Compile-time layout of one net in the packed-SGPR region (must match
-// derive_shape's sp_lin_off and cnf_prepare's mode 3).
-template <int D, int H1, int H2>
-struct SP {
-  static constexpr int DT = D / 2, DC = D - D / 2;
-  static constexpr int NL = H1 == 0 ? 1 : (H2 == 0 ? 2 : 3);
-  static constexpr int nin(int i) { return i == 0 ? DC : (i == 1 ? H1 : H2); }
-  static constexpr int nout(int i) { return i == NL - 1 ? DT : (i == 0 ? H1 : H2); }
-  // per output row: [w_o0, b_o, w_o1 .. w_o(nin-1)], row stride even so that
-  // (w_o0, b_o) is one aligned SGPR pair
-  static constexpr int stride(int i) { return (nin(i) + 2) & ~1; }
-  static constexpr int fl(int i) { return pad16(nout(i) * stride(i)); }
-  static constexpr int off(int i) { return i == 0 ? 0 : off(i - 1) + fl(i - 1); }
-  static constexpr int NF = off(NL);
-  static constexpr int mx(int i) { return i == NL ? 0 : (fl(i) > mx(i + 1) ? fl(i) : mx(i + 1)); }
-  static constexpr int NC = mx(0) / 16;  // 64-B chunks per buffer
-  static_assert(NC >= 1 && NC <= 2, "Linear block exceeds the 32-float SGPR buffer");
-};
-
-template <int NC>
-struct SW {
-  v16f c[NC];
-  __device__ __forceinline__ float operator[](int i) const { return c[i >> 4][i & 15]; }
-  __device__ __forceinline__ f2 pair(int i) const {  // i even
-    return f2{c[i >> 4][i & 15], c[i >> 4][(i & 15) + 1]};
-  }
-};
-
-// w0 * x + b with (w0, b) ONE SGPR pair: op_sel broadcasts the low half as the
-// multiplier and the high half as the addend, so the bias costs no VALU move.
-__device__ __forceinline__ f2 fma_wb(f2 wb, f2 x) {
-  f2 a;
-  asm("v_pk_fma_f32 %0, %1, %2, %1 op_sel:[0,0,1] op_sel_hi:[0,1,1]" : "=v"(a) : "s"(wb), "v"(x));
-  return a;
-}
-// ... and the clamped forms that end a hidden neuron (relu folded, see header)
-__device__ __forceinline__ f2 fma_wb_clamp(f2 wb, f2 x) {
-  f2 a;
-  asm("v_pk_fma_f32 %0, %1, %2, %1 op_sel:[0,0,1] op_sel_hi:[0,1,1] clamp"
-      : "=v"(a) : "s"(wb), "v"(x));
-  return a;
-}
-__device__ __forceinline__ f2 fma_clamp(float w, f2 x, f2 acc) {
-  f2 a;
-  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1] clamp" : "=v"(a) : "s"(f2{w, w}), "v"(x),
-      "v"(acc));
-  return a;
-}
-
-// Weight-block loads.  Each Linear's block arrives in SGPRs one Linear ahead:
-//   sready()          wait for the block issued one Linear ago -- a
-//                     compiler-visible s_waitcnt lgkmcnt(0), so the compiler
-//                     adds no wait of its own before the block's first use
-//                     (scalar loads return out of order: any later wait
-//                     would be lgkmcnt(0) and would also wait for the block
-//                     issued next);
-//   sissue(next, p)   then issue the next block, before this Linear's FMAs.
-// Plain (compiler-visible) loads: the waitcnt pass guards every read of the
-// destination SGPRs, copies and spills included.  The sched_barriers pin the
-// order wait -> issue -> FMAs, and leave each Linear's neurons one scheduling
-// region.  (An inline-asm load/wait pair let the register allocator copy
-// still-in-flight SGPRs.)
-__device__ __forceinline__ void sready() {
-  __builtin_amdgcn_sched_barrier(0);
-  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0); vmcnt, expcnt untouched (gfx9 encoding)
-  __builtin_amdgcn_sched_barrier(0);
-}
-template <int NC>
-__device__ __forceinline__ void sissue(SW<NC>& r, const float* p) {
-  const v16f* q = reinterpret_cast<const v16f*>(__builtin_assume_aligned(p, 64));
-#pragma unroll
-  for (int i = 0; i < NC; ++i) r.c[i] = q[i];
-  __builtin_amdgcn_sched_barrier(0);
-}
 
 // Conditioner activations of the lane's P row pairs (pair-major).
 template <int D, int H1, int H2, int P>
@@ -317,114 +243,6 @@ __device__ __forceinline__ void sp_step(f2 (&v)[P][D], f2 (&ld)[P], SW<SP<D, H1,
 // tile I/O: a lane's 2P rows (pairs p = rows 2P*l + 2p, +1) are the 2*P*D
 // contiguous floats at row 2P*l of the wave's tile
 // ---------------------------------------------------------------------------
-// HBM -> LDS copy of one full wave tile (TR*D floats, 16-B aligned) by
-// LDS-DMA: one global_load_lds_dwordx4 moves 1 KiB, lane-linear.
-template <int D, int TR>
-__device__ __forceinline__ void wave_dma(float* sm, const float* __restrict__ src, int lane) {
-  constexpr int N4 = TR * D / 4, NI = (N4 + 63) / 64;
-#pragma unroll
-  for (int i = 0; i < NI; ++i) {
-    if (N4 % 64 == 0 || i * 64 + lane < N4)
-      __builtin_amdgcn_global_load_lds(src + (i * 64 + lane) * 4,
-                                       (__attribute__((address_space(3))) void*)(sm + i * 256), 16,
-                                       0, 0);
-  }
-}
-
-// the lane's pairs from the LDS tile (one ds_read2_b32 per feature and pair)
-template <int D, int P>
-__device__ __forceinline__ void read_pairs(const float* sm, int lane, f2 (&v)[P][D]) {
-  const float* b = sm + 2 * P * D * lane;
-#pragma unroll
-  for (int p = 0; p < P; ++p)
-#pragma unroll
-    for (int k = 0; k < D; ++k) v[p][k] = f2{b[2 * p * D + k], b[(2 * p + 1) * D + k]};
-}
-
-// The lane's 2*P*D output floats (pairs in logical order) to dst = its first
-// row: 16-B stores when aligned, else 8-B, else 4-B; `rows` < 2P on the ragged
-// tile.
-template <int D, int P>
-__device__ __forceinline__ void store_rows(float* __restrict__ dst, const f2 (&v)[P][D], int rows,
-                                           int al) {
-  constexpr int NF = 2 * P * D;
-  float r[NF];
-#pragma unroll
-  for (int p = 0; p < P; ++p)
-#pragma unroll
-    for (int k = 0; k < D; ++k) {
-      r[2 * p * D + k] = v[p][k].x;
-      r[(2 * p + 1) * D + k] = v[p][k].y;
-    }
-  if (rows == 2 * P && NF % 4 == 0 && al >= 16) {
-#pragma unroll
-    for (int q = 0; q < NF / 4; ++q)
-      reinterpret_cast<float4*>(dst)[q] = float4{r[4 * q], r[4 * q + 1], r[4 * q + 2], r[4 * q + 3]};
-  } else if (rows == 2 * P && NF % 2 == 0 && al >= 8) {
-#pragma unroll
-    for (int q = 0; q < NF / 2; ++q) reinterpret_cast<float2*>(dst)[q] = float2{r[2 * q], r[2 * q + 1]};
-  } else {
-#pragma unroll
-    for (int k = 0; k < NF; ++k)
-      if (k < rows * D) dst[k] = r[k];
-  }
-}
-
-template <int P>
-__device__ __forceinline__ void store_lds(float* __restrict__ dst, const f2 (&ld)[P], int rows,
-                                          int al) {
-  if (P == 2 && rows == 4 && al >= 16) {
-    *reinterpret_cast<float4*>(dst) = float4{ld[0].x, ld[0].y, ld[P - 1].x, ld[P - 1].y};
-  } else if (rows == 2 * P && al >= 8) {
-#pragma unroll
-    for (int p = 0; p < P; ++p) reinterpret_cast<float2*>(dst)[p] = float2{ld[p].x, ld[p].y};
-  } else {
-#pragma unroll
-    for (int p = 0; p < P; ++p) {
-      if (2 * p < rows) dst[2 * p] = ld[p].x;
-      if (2 * p + 1 < rows) dst[2 * p + 1] = ld[p].y;
-    }
-  }
-}
-
-// reverse the logical order of a row held in orientation 1 (odd L): afterwards
-// v[j] is logical j, so the epilogues have one form
-template <int D>
-__device__ __forceinline__ void unflip(f2* v) {
-#pragma unroll
-  for (int k = 0; k < D / 2; ++k) {
-    const f2 a = v[k];
-    v[k] = v[D - 1 - k];
-    v[D - 1 - k] = a;
-  }
-}
-
-// Labels of the lane's rows (int64 each, 16-B loads when aligned), packed one
-// byte per row into ONE register so they cost no VGPRs across the layer sweep.
-// A label is valid iff 0 <= y < D; an invalid one (byte 0xff) poisons the loss
-// terms with NaN (the reference's probs.gather raises on it).  rows: valid rows.
-template <int D, int P>
-__device__ __forceinline__ uint32_t load_labels(const int64_t* __restrict__ y, int rows,
-                                                bool al16) {
-  uint32_t packed = 0;
-  const int32_t* y32 = reinterpret_cast<const int32_t*>(y);
-#pragma unroll
-  for (int p = 0; p < P; ++p) {
-    int lo0 = 0, hi0 = 0, lo1 = 0, hi1 = 0;
-    if (rows == 2 * P && al16) {
-      const int4 q = reinterpret_cast<const int4*>(y32)[p];
-      lo0 = q.x, hi0 = q.y, lo1 = q.z, hi1 = q.w;
-    } else {
-      if (2 * p < rows) lo0 = y32[4 * p], hi0 = y32[4 * p + 1];
-      if (2 * p + 1 < rows) lo1 = y32[4 * p + 2], hi1 = y32[4 * p + 3];
-    }
-    const uint32_t b0 = hi0 == 0 && (unsigned)lo0 < (unsigned)D ? (uint32_t)lo0 : 0xffu;
-    const uint32_t b1 = hi1 == 0 && (unsigned)lo1 < (unsigned)D ? (uint32_t)lo1 : 0xffu;
-    packed |= (b0 | (b1 << 8)) << (16 * p);
-  }
-  return packed;
-}
-
 // Loss terms of one pair's rows (logical order):
 // CAL: loss = -(log(softmax(z)[y] + 1e-7) + ld)    calibrators.py:288-291
 // CE:  loss = -log_softmax(z)[y] - det * ld         run_experiment3D.py:107

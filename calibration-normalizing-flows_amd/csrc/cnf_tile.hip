@@ -440,6 +440,15 @@ int prepare_run(const Shape& s, const float* const* params, void* prepared, hipS
         g.dst = d2 + (k / s.n_lin) * s.sp_net_floats + s.sp_lin_off[i];
       }
       hipLaunchKernelGGL(k_prepare, dim3(b.nseg), dim3(256), 0, st, b, wreg, idx);
+      // ... and a plain copy (no relu or log2(e) scaling) for the reverse mode
+      PrepArgs c = b;
+      const int64_t d3 = s.vp_region + (int64_t)l * s.sp_net_floats * s.nets;
+      for (int k = 0; k < c.nseg; ++k) {
+        PrepSeg& g = c.seg[k];
+        g.wmul = g.bmul = 1.f;
+        g.dst = d3 + (k / s.n_lin) * s.sp_net_floats + s.sp_lin_off[k % s.n_lin];
+      }
+      hipLaunchKernelGGL(k_prepare, dim3(c.nseg), dim3(256), 0, st, c, wreg, idx);
     }
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) {
