@@ -42,7 +42,10 @@ WORKLOADS = {
     # name: (D, L, hidden, B per GPU, inverse)
     "cfg1": dict(D=3, L=2, hidden=[5, 5], B=4096, scale=False, inverse=False),
     "cfg2": dict(D=10, L=6, hidden=[5, 5], B=1 << 20, scale=True, inverse=False),
-    "cfg4": dict(D=100, L=12, hidden=[100, 100], B=1 << 18, scale=True, inverse=False),
+    # cfg4: the reference's own Linear init (N(0, 0.1) on 100-wide Linears
+    # overflows exp(s) within a few layers: inf / NaN everywhere)
+    "cfg4": dict(D=100, L=12, hidden=[100, 100], B=1 << 18, scale=True, inverse=False,
+                 sigma=None),
     "cfg5": dict(D=10, L=6, hidden=[5, 5], B=1 << 20, scale=True, inverse=True),
 }
 
@@ -92,10 +95,11 @@ def make_flow(w, device, seed=0):
     np.random.seed(seed)
     flow = Flow([NvpCouplingLayer(w["D"], w["hidden"], scale=w["scale"]) for _ in range(w["L"])])
     g = torch.Generator().manual_seed(seed)
+    sigma = w.get("sigma", 0.1)
     with torch.no_grad():
         for p in flow.parameters():
-            if p.requires_grad:  # N(0, 0.1): SURVEY 8(d) synthetic weights
-                p.copy_(torch.randn(p.shape, generator=g) * 0.1)
+            if p.requires_grad and sigma is not None:  # N(0, 0.1): SURVEY 8(d) synthetic weights
+                p.copy_(torch.randn(p.shape, generator=g) * sigma)
     return flow.to(device)
 
 
@@ -207,11 +211,14 @@ def kernel_only_seconds(runner, launches):
     return t / launches
 
 
-def train_step_rate(dev, B=1 << 20, steps=20):
+def train_step_rate(dev, workload="cfg2", B=None, steps=20):
     """Fused calibrator training step (cnf_loss_vjp: forward + loss + reverse
-    mode + fixed-order gradient reduction) on the cfg2 shape: vectors/s."""
+    mode + fixed-order gradient reduction) on a workload's shape: vectors/s.
+    Algorithmic training flops = 3x the forward's (forward, input gradients,
+    weight gradients); the reverse mode's recompute is not counted."""
     from cnf_hip import vjp as V
-    w = WORKLOADS["cfg2"]
+    w = WORKLOADS[workload]
+    B = B or w["B"]
     flow = make_flow(w, dev)
     stack = flow._native_stack()
     x, y = synthetic_logits(B, w["D"], dev, 4321)
@@ -225,7 +232,10 @@ def train_step_rate(dev, B=1 << 20, steps=20):
     e1.record()
     torch.cuda.synchronize(dev)
     t = e0.elapsed_time(e1) / 1e3 / steps
+    tf = 3 * algo_flops_per_vec(w["D"], w["L"], w["hidden"], w["scale"]) * B / t / 1e12
+    peak = MFMA_F32_PEAK_TFLOPS if w["D"] >= 32 else VALU_PEAK_TFLOPS
     return {"vec_per_s": round(B / t, 1), "ms_per_step": round(t * 1e3, 4), "B": B,
+            "tflops": round(tf, 2), "frac": round(tf / peak, 4),
             "note": "forward + calibrator loss + VJP + gradient reduction; optimizer excluded"}
 
 
@@ -397,12 +407,13 @@ def main():
             fv = algo_flops_per_vec(wl["D"], wl["L"], wl["hidden"], wl["scale"])
             rf = roofline(wl["B"], bv, fv, ka, mfma=wl["D"] >= 32)
             variants[name] = {"vec_per_s": round(wl["B"] / ka, 1), "kernel_avg_us": round(ka * 1e6, 2),
-                              "B": wl["B"], "kernel": r.stack.kernel_name(),
+                              "B": wl["B"], "kernel": r.stack.kernel_name(allo),
                               "hbm_gbs": rf["hbm_gbs"], "tflops": rf["compute_tflops"],
                               "bound": rf["bound"], "frac": rf["frac"]}
             del r
             torch.cuda.empty_cache()
         variants["cfg2_train_step_fused_loss_vjp"] = train_step_rate(dev)
+        variants["cfg4_train_step_loss_vjp"] = train_step_rate(dev, "cfg4", steps=5)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -424,7 +435,8 @@ def main():
                                                   w["hidden"], w["B"],
                                                   ", inverse" if w["inverse"] else ""),
                        "global_batch": w["B"] * world, "parallelism": "dp%d" % world,
-                       "hidden_size": w["hidden"], "weights": "N(0,0.1) synthetic"},
+                       "hidden_size": w["hidden"], "weights": ("N(0,%g) synthetic" % w.get("sigma", 0.1)) if w.get("sigma", 0.1) is not None
+                       else "the reference's default Linear init (synthetic)"},
             "roofline": roof,
         "step": "fused forward + log-det + NLL sums (cnf_forward_loss)%s" % (
             " + RCCL all-reduce of the NLL sums" if world > 1 else "") if mode == "loss"

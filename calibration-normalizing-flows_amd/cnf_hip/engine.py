@@ -108,8 +108,11 @@ class CouplingStack:
         return all(ly.dim == l0.dim and list(ly.hidden_size) == list(l0.hidden_size)
                    and ly.scale == l0.scale and ly.shift == l0.shift for ly in layers)
 
-    def kernel_name(self):
-        return _lib.lib().cnf_kernel_name(ctypes.byref(self.desc)).decode()
+    def kernel_name(self, all_outputs=False):
+        """Kernel family serving this stack; every-layer-output calls of an
+        sgpr-fused stack run on valu-fused (cnf_valu.hip valu_run)."""
+        name = _lib.lib().cnf_kernel_name(ctypes.byref(self.desc)).decode()
+        return "valu-fused" if all_outputs and name == "sgpr-fused" else name
 
     def param_tensors(self):
         """ABI order (include/cnf.h cnf_param_tensor_count)."""

@@ -135,7 +135,7 @@ int cnf_prepared_bytes(const cnf_desc* desc, size_t* bytes) {
   if (st != CNF_OK) return st;
   if (!bytes) return CNF_ERR_NULL;
   const int64_t wf = s.family == Family::kTile
-                       ? s.tile_layer_floats * s.L + s.wide_floats
+                       ? s.tile_layer_floats * s.L + s.wide_floats + s.layer_floats * s.L
                        : s.valu_net_floats * s.nets * s.L +
                              (s.sp_ok ? 2 * s.sp_net_floats * s.nets * s.L : 0);
   // +256: scalar-cache prefetch reads whole 64-B lines past the last weight

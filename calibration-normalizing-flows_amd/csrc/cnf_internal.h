@@ -56,6 +56,9 @@ struct Shape {
   // register-resident MFMA layout (cnf_wide.hip), appended after the tile region
   int64_t wide_region = 0;           // float offset of the region in the weights region
   int64_t wide_floats = 0;           // floats of the region (0: shape not in its table)
+  // natural (state_dict order) copy of every parameter, after the wide region:
+  // the reverse mode's operands (cnf_wvjp.hip)
+  int64_t plain_region = 0;
 };
 
 // Prepared blob: [int32 fwd_q L*D][int32 inv_q L*D][int32 flags L] padded to
@@ -98,6 +101,14 @@ bool wide_ok(const Shape& s);               // k_wide serves this descriptor's f
 int wide_prepare(const Shape& s, const float* const* params, void* prepared, hipStream_t st);
 int wide_run(const Shape& s, const void* prepared, const float* in, float* out, float* ld,
              int64_t B, bool inverse, hipStream_t st);
+
+// layer-at-a-time MFMA reverse mode of the tile family (cnf_wvjp.hip)
+bool wvjp_ok(const Shape& s);
+int wvjp_workspace(const Shape& s, int64_t B, size_t* bytes);
+int wvjp_run(const Shape& s, const void* prepared, const float* x, const int64_t* y,
+             const float* gz, const float* gz_all, const float* gld, int kind, float det,
+             float grad_scale, float* loss_terms, float* grads, float* dx, int64_t B, void* ws,
+             size_t ws_bytes, hipStream_t st);
 
 int vjp_workspace(const Shape& s, int64_t B, size_t* bytes);
 bool vjp2_ok(const Shape& s);  // the packed-pair SGPR reverse-mode kernel serves this shape

@@ -335,6 +335,7 @@ int tile_configure(Shape* s) {
   s->tile_lds_bytes = per_wave * waves;
   s->wide_region = s->tile_layer_floats * s->L;
   s->wide_floats = wide_layer_floats(*s) * s->L;
+  s->plain_region = s->wide_region + s->wide_floats;
   return CNF_OK;
 }
 
@@ -418,6 +419,18 @@ int prepare_run(const Shape& s, const float* const* params, void* prepared, hipS
       a.iq[j] = perm ? s.D - 1 - rev[j] : s.D - 1 - j;
     }
     hipLaunchKernelGGL(k_prepare, dim3(a.nseg + 1), dim3(256), 0, st, a, wreg, idx);
+    if (tiled) {
+      // natural copy of the layer (state_dict order) for the reverse mode
+      PrepArgs c = a;
+      int64_t d = s.plain_region + (int64_t)l * s.layer_floats;
+      for (int k = 0; k < c.nseg; ++k) {
+        PrepSeg& g = c.seg[k];
+        g.mode = 0;
+        g.dst = d;
+        d += (int64_t)g.nout_full * g.nin_full + g.nout_full;
+      }
+      hipLaunchKernelGGL(k_prepare, dim3(c.nseg), dim3(256), 0, st, c, wreg, idx);
+    }
     if (!tiled && s.sp_ok) {
       // second copy of the layer in the packed SGPR layout (no index block)
       PrepArgs b = a;

@@ -310,7 +310,9 @@ int valu_run(const Shape& s, const void* prepared, const float* in, float* out, 
              float* loss_ws, int kind, float det, float* loss_terms) {
   if (s.valu_id < 0) return CNF_ERR_UNSUPPORTED;
   if (B == 0) return CNF_OK;
-  if (sgpr_enabled(s)) {
+  // every-layer outputs (all != null) stay on k_valu: its LDS-staged stores
+  // write the L*B*D floats at ~4.2 TB/s, k_sgpr's per-lane ones at ~3 TB/s
+  if (sgpr_enabled(s) && all == nullptr) {
     const int r = sgpr_run(s, prepared, in, out, ld, all, B, inverse, st, y, loss_ws, kind, det,
                            loss_terms);
     if (r != CNF_ERR_UNSUPPORTED) return r;

@@ -1239,6 +1239,7 @@ size_t v2_stash_offset(const Shape& s, int64_t nblk) {
 }
 
 int vjp_workspace(const Shape& s, int64_t B, size_t* bytes) {
+  if (s.family == Family::kTile) return wvjp_workspace(s, B, bytes);
   if (const V2Entry* e2 = find_v2(s)) {
     // the larger of the two variants (loss / generic) -- same grid rule
     const int64_t g = std::max(grid_v2(s, pick_v2(e2, s, true), B),
@@ -1256,6 +1257,9 @@ int vjp_run(const Shape& s, const void* prepared, const float* x, const int64_t*
             const float* gz, const float* gz_all, const float* gld, int kind, float det,
             float grad_scale, float* loss_terms, float* grads, float* dx, int64_t B, void* ws,
             size_t ws_bytes, hipStream_t st) {
+  if (s.family == Family::kTile)
+    return wvjp_run(s, prepared, x, y, gz, gz_all, gld, kind, det, grad_scale, loss_terms, grads,
+                    dx, B, ws, ws_bytes, st);
   if (const V2Entry* e2 = find_v2(s)) {
     size_t need = 0;
     int r = vjp_workspace(s, B, &need);

@@ -1,0 +1,796 @@
+// Reverse mode for the MFMA family (every shape outside the VALU tables: D > 16,
+// or wider / deeper conditioners): cnf_vjp / cnf_loss_vjp for cfg4-class flows.
+//
+// Replaces autograd of flows/flows.py:101-112 (NvpCouplingLayer.forward),
+// flows/utils.py:26-31 (MLP.forward) and the calibrator losses
+// (calibrators.py:287-291, run_experiment3D.py:102-107) for these shapes.
+//
+// Unlike k_vjp2 (a lane owns two rows through all L layers), a wide conditioner
+// (cfg4: three 100-wide Linears per net, 12 layers, 727 K parameters) does not
+// fit a row-resident sweep: its weight gradients are GEMMs whose reduction
+// dimension is the batch.  So the reverse mode runs layer at a time over the
+// whole batch, every product on v_mfma_f32_32x32x2_f32 (exact f32):
+//
+//   forward   per layer: the conditioner Linears (one launch per Linear, both
+//             nets as grid.z; bias + ReLU fused into the epilogue), then the
+//             coupling update + flip/permutation gather + log-det (one wave per
+//             row).  Every layer's output is stashed (HBM: 288 GB leaves room),
+//             so no inverse is needed.
+//   seed      the loss (softmax-NLL / CE and its gradient) or the caller's
+//             upstream gradients, per row; loss sums in fixed block order.
+//   backward  per layer, last first: recompute the conditioner activations
+//             from the stashed input, back through the coupling update (one
+//             wave per row), back through the Linears (G_{k-1} = (G_k W_k) *
+//             relu'(H_{k-1}); the first Linear's input gradient of both nets
+//             is added into the conditioning half in one launch), then ONE
+//             launch computing every Linear's weight and bias gradient as
+//             G_k^T [H_{k-1} | 1] over row blocks (per-block partials summed
+//             in block order: deterministic).
+//
+// Activation layout (workspace, row-major, every leading dimension a multiple
+// of 8 floats, so A panels load as float4 and a panel's 8-wide groups never
+// leave the row):
+//   stash row  [x_C (DC) | 1 | 0 pad to Cp][x_T (DT) | 0 pad to DTp]  (Dp floats)
+//              conditioning half first: the first Linear's operand starts the
+//              row, and its ones column gives the bias gradient for free;
+//   H_k row    [relu(h) (units) | 1 | 0 pad]   (Hp_k floats);
+//   G_k row    [grad (nout) | 0 pad]           (Gp_k floats);
+//   gradients of the layer outputs stay in the caller's natural [B][D] order.
+// Pad columns are written (zeros / ones), never left uninitialised: the GEMMs
+// read them and multiply them by zero weight rows.
+//
+// Every launch is a plain kernel on the caller's stream; no host sync.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "cnf_internal.h"
+
+namespace cnf {
+namespace {
+
+using f16v = __attribute__((ext_vector_type(16))) float;
+using f4 = __attribute__((ext_vector_type(4))) float;
+
+constexpr int kBN = 64;      // output columns per GEMM block (2 MFMA tiles of 32)
+constexpr int kKC = 128;     // reduction chunk a wave holds in registers (16 x float4)
+constexpr int kDwCols = 64;  // gradient columns per k_wdw wave (2 MFMA tiles)
+
+inline int r8(int n) { return (n + 7) & ~7; }
+
+enum Epi { kEpiBias = 0, kEpiBiasRelu = 1, kEpiMask = 2, kEpiAdd = 3 };
+
+// C[m][n] = epi(sum_k A[m][k] B(k, n)); B(k, n) = Bw[n*ldb + k] (BT: a Linear's
+// forward, W[out][in]) or Bw[k*ldb + n] (its transpose product, back-prop).
+// Columns N <= n < ldw are pad: 1 at n == N when ones, else 0.
+struct GemmJob {
+  const float* A;
+  const float* Bw;
+  const float* A2;    // PAIR: C = A Bw + A2 Bw2 (both nets into one output)
+  const float* Bw2;
+  const float* bias;  // [N]        kEpiBias, kEpiBiasRelu
+  const float* mask;  // [M][ldm]   kEpiMask: C *= (mask > 0), relu'
+  float* C;
+  int64_t lda, lda2, ldm, ldc;
+  int ldb, ldb2, N, K, ldw, ones;
+};
+struct GemmArgs {
+  GemmJob job[2];  // one per conditioner net (grid.z)
+  int64_t M;
+};
+
+// A's reduction chunk [kc, kc + 128) of one 32-row panel (lane: row r, half
+// h): group g holds k = kc + 8g + 4h .. +3, one float4.  Rows past M read the
+// last row (those outputs are never stored).  Leading dimensions are padded
+// to 8 with written pad (zeros / the ones column), so the groups covering K
+// stay inside the row and meet zero weight rows past K; a group past the row
+// (only in a chunk's unused tail) reads a clamped in-row address.  No lane branches, no use of a
+// loaded value before the MFMAs: the loads stay in flight.
+__device__ __forceinline__ void load_panel(f4 (&a)[16], const float* __restrict__ A, int64_t lda,
+                                           int64_t row, int64_t M, int kc, int kmax, int h) {
+  const float* arow = A + (row < M ? row : M - 1) * lda;
+#pragma unroll
+  for (int g = 0; g < 16; ++g)
+    a[g] = *reinterpret_cast<const f4*>(arow + min(kc + 8 * g + 4 * h, kmax));
+}
+
+// acc[c] += A_panel . W[kc.., c-th 32 columns] for the chunk's ng groups; the
+// LDS reads of group g+1 are issued before group g's MFMAs.  In step e of
+// group g lane half h supplies k = 8g + 4h + e for A and for B alike (a
+// permuted summation order, the same products).
+template <int NC>
+__device__ __forceinline__ void panel_mfma(f16v (&acc)[4], const f4 (&a)[16], const float* Wq,
+                                           int ST, int kc, int ng, int r, int h) {
+  float b[2][4][NC];  // ping-pong by group parity: no register copies
+  auto ldb = [&](int g, float (&bb)[4][NC]) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float* wrow = Wq + (kc + 8 * g + 4 * h + e) * ST + r;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) bb[e][c] = wrow[c * 32];
+    }
+  };
+  ldb(0, b[0]);
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+    if (g < ng) {
+      if (g + 1 < ng) ldb(g + 1, b[(g + 1) & 1]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+          acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[g][e], b[g & 1][e][c], acc[c], 0, 0, 0);
+    }
+  }
+}
+
+// The GEMM: the block stages its 32*NC-column slice of the weights (both,
+// PAIR) in LDS ONCE, then each wave streams 32-row panels of A straight from
+// HBM into registers (16-B loads, no LDS round trip, no barrier).  64-column
+// blocks keep the wave at ~124 registers and the weight slice at ~30 KB, so
+// four blocks share a CU (four waves per SIMD): a wave's panel loads and
+// epilogue hide under the others' MFMAs.  (A register-prefetched next panel at one wave per SIMD measured
+// slower: the compiler sinks the prefetch back next to its MFMAs.)  LDS row
+// stride 32*NC + 8 puts the two lane halves' rows (4 apart)
+// on disjoint banks.
+template <bool BT, int EPI, bool PAIR, int NC>
+__global__ __launch_bounds__(256, PAIR ? 3 : 4) void k_wgemm(GemmArgs ga) {
+  const GemmJob& j = ga.job[blockIdx.z];
+  extern __shared__ __attribute__((aligned(16))) float Ws[];
+  const int t = threadIdx.x, lane = t & 63, r = lane & 31, h = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int n0 = blockIdx.y * kBN, N = j.N, K = j.K;
+  constexpr int Nt = NC * 32, ST = Nt + 8;
+  const int Kp = (K + 7) & ~7;
+  // weight slice -> LDS, 8 loads in flight per thread (a dependent load-store
+  // loop would pay the full memory latency per element)
+#pragma unroll
+  for (int q = 0; q < (PAIR ? 2 : 1); ++q) {
+    const float* Bw = q ? j.Bw2 : j.Bw;
+    const int ldb = q ? j.ldb2 : j.ldb;
+    float* dst = Ws + q * Kp * ST;
+    const int total = Kp * Nt;
+    for (int i0 = 0; i0 < total; i0 += 256 * 8) {
+      float v[8];
+      int at[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + u * 256 + t;
+        int k, n;
+        if (BT) {
+          k = i % Kp;
+          n = i / Kp;
+        } else {
+          n = i % Nt;
+          k = i / Nt;
+        }
+        const int nn = n0 + n;
+        const bool ok = i < total && k < K && nn < N;
+        const int64_t src = ok ? (BT ? (int64_t)nn * ldb + k : (int64_t)k * ldb + nn) : 0;
+        v[u] = Bw[src];
+        v[u] = ok ? v[u] : 0.f;
+        at[u] = i < total ? k * ST + n : -1;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (at[u] >= 0) dst[at[u]] = v[u];
+    }
+  }
+  __syncthreads();
+  const int64_t M = ga.M, panels = (M + 31) >> 5, stride = (int64_t)gridDim.x * 4;
+  auto epilogue = [&](const f16v (&acc)[4], int64_t m0) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int n = n0 + c * 32 + r;
+      if (n >= j.ldw) continue;
+      const bool real = n < N;
+      const float pad = (j.ones && n == N) ? 1.f : 0.f;
+      const float b = (EPI == kEpiBias || EPI == kEpiBiasRelu) && real ? j.bias[n] : 0.f;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int64_t m = m0 + (q & 3) + 8 * (q >> 2) + 4 * h;
+        if (m >= M) continue;
+        float v = acc[c][q];
+        if constexpr (EPI == kEpiBias || EPI == kEpiBiasRelu) v += b;
+        if constexpr (EPI == kEpiBiasRelu) v = v < 0.f ? 0.f : v;  // keeps NaN (torch relu)
+        if constexpr (EPI == kEpiMask) v = real && j.mask[m * j.ldm + n] > 0.f ? v : 0.f;
+        if constexpr (EPI == kEpiAdd) v += j.C[m * j.ldc + n];
+        j.C[m * j.ldc + n] = real ? v : pad;
+      }
+    }
+  };
+  int64_t pn = (int64_t)blockIdx.x * 4 + w;
+  for (; pn < panels; pn += stride) {
+    f16v acc[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[c] = f16v{};
+#pragma unroll
+    for (int q = 0; q < (PAIR ? 2 : 1); ++q) {
+      const float* A = q ? j.A2 : j.A;
+      const int64_t lda = q ? j.lda2 : j.lda;
+      for (int kc = 0; kc < Kp; kc += kKC) {
+        f4 a[16];
+        load_panel(a, A, lda, pn * 32 + r, M, kc, (int)(lda - 4), h);
+        panel_mfma<NC>(acc, a, Ws + q * Kp * ST, ST, kc, min(16, (Kp - kc) >> 3), r, h);
+      }
+    }
+    epilogue(acc, pn * 32);
+  }
+}
+
+// Weight gradients: one wave per block owns a 32 (outputs) x 32*NC (inputs and
+// the ones column) strip of one (net, Linear) job over the block's row range,
+// written into the block's partial record in state_dict layout (so the
+// reduction is one fixed-order column sum).  Both MFMA operands come straight
+// from HBM: in k-step s, lane (i, h) reads G[row][n0 + i] and
+// H[row][c0 + 32c + i] of batch row mr + 2s + h -- 128 contiguous bytes per
+// half-wave.  Out-of-range outputs read clamped addresses and are never
+// written; only the batch's last partial chunk masks rows.  The next 32 rows'
+// operands load under this chunk's MFMAs.
+struct DwJob {
+  const float* G;
+  const float* H;
+  int64_t ldg, ldh;
+  int64_t woff, boff;  // float offsets of W[0][in_off] and b[0] in the layer record
+  int wld, N, K, tiles_k;
+};
+struct DwArgs {
+  DwJob job[2 * kMaxLin];
+  float* partials;  // [nkb][PS]
+  int64_t M, rows, PS;
+};
+
+template <int NC>
+__global__ __launch_bounds__(64) void k_wdw(DwArgs da) {
+  const DwJob& j = da.job[blockIdx.y];
+  const int lane = threadIdx.x, i = lane & 31, h = lane >> 5;
+  const int nsub = (j.N + 31) >> 5;
+  const int ns = (int)blockIdx.z % nsub, ct = (int)blockIdx.z / nsub;
+  if (ct >= j.tiles_k) return;
+  const int n0 = ns * 32, c0 = ct * 32 * NC;
+  const int64_t r0 = (int64_t)blockIdx.x * da.rows;
+  const int64_t r1 = min(da.M, r0 + da.rows);
+  if (r0 >= r1) return;
+  const float* gcol = j.G + min(n0 + i, j.N - 1);
+  const float* hcol[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) hcol[c] = j.H + min(c0 + 32 * c + i, (int)j.ldh - 1);
+  auto load = [&](int64_t mr, float (&a)[16], float (&b)[NC][16]) {
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int64_t row = mr + 2 * s + h;
+      a[s] = gcol[row * j.ldg];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) b[c][s] = hcol[c][row * j.ldh];
+    }
+  };
+  f16v acc[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) acc[c] = f16v{};
+  const int64_t rfull = r0 + (r1 - r0) / 32 * 32;  // rows in whole chunks
+  if (rfull > r0) {
+    float a[16], b[NC][16];
+    load(r0, a, b);
+    for (int64_t mr = r0; mr < rfull; mr += 32) {
+      float an[16], bn[NC][16];
+      load(mr + 32 < rfull ? mr + 32 : mr, an, bn);
+      __builtin_amdgcn_sched_barrier(0);  // next chunk's loads stay ahead of the MFMAs
+#pragma unroll
+      for (int s = 0; s < 16; ++s)
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+          acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[c][s], acc[c], 0, 0, 0);
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        a[s] = an[s];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) b[c][s] = bn[c][s];
+      }
+    }
+  }
+  if (rfull < r1) {  // the batch's ragged end: rows past r1 contribute zero
+    float a[16], b[NC][16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int64_t row = rfull + 2 * s + h;
+      const bool ok = row < r1;
+      const int64_t rr = ok ? row : r1 - 1;
+      a[s] = ok ? gcol[rr * j.ldg] : 0.f;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) b[c][s] = hcol[c][rr * j.ldh];
+    }
+#pragma unroll
+    for (int s = 0; s < 16; ++s)
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+        acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[c][s], acc[c], 0, 0, 0);
+  }
+  float* out = da.partials + (int64_t)blockIdx.x * da.PS;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int k = c0 + c * 32 + i;
+    if (k > j.K) continue;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int nn = n0 + (q & 3) + 8 * (q >> 2) + 4 * h;
+      if (nn >= j.N) continue;
+      if (k < j.K) out[j.woff + (int64_t)nn * j.wld + k] = acc[c][q];
+      else out[j.boff + nn] = acc[c][q];
+    }
+  }
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Row geometry of the stash layout (see the file comment).
+struct Geo {
+  int D, DT, DC, Cp, DTp, Dp;
+  __device__ __forceinline__ int col(int i) const { return i < DT ? Cp + i : i - DT; }
+};
+
+// Natural [B][D] rows -> stash layout (the first layer's input).
+__global__ __launch_bounds__(256) void k_wstash(const float* __restrict__ x,
+                                                float* __restrict__ xs, int64_t B, Geo g) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < B; r += nw) {
+    for (int c = lane; c < g.Dp; c += 64) {
+      float v;
+      if (c < g.DC) v = x[r * g.D + g.DT + c];
+      else if (c == g.DC) v = 1.f;
+      else if (c >= g.Cp && c < g.Cp + g.DT) v = x[r * g.D + c - g.Cp];
+      else v = 0.f;
+      xs[r * g.Dp + c] = v;
+    }
+  }
+}
+
+// Coupling update of one layer (flows/flows.py:101-112), one wave per row:
+//   z_i = x_i e^{s_i} + t_i (i < DT), x_i otherwise; ld += sum_i s_i;
+//   out[j] = z[fq[j]] (permutation, then flip); stash layout in and out.
+__global__ __launch_bounds__(256) void k_wfwd_update(const float* __restrict__ X,
+                                                     float* __restrict__ Xn, float* __restrict__ ld,
+                                                     const float* __restrict__ Os,
+                                                     const float* __restrict__ Ot,
+                                                     const int32_t* __restrict__ fq, int64_t B,
+                                                     Geo g, int first) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < B; r += nw) {
+    const float* xr = X + r * g.Dp;
+    float* zr = Xn + r * g.Dp;
+    float sacc = 0.f;
+    for (int j = lane; j < g.D; j += 64) {
+      const int i = fq[j];
+      float v = xr[g.col(i)];
+      if (i < g.DT) {
+        const float s = Os ? Os[r * g.DTp + i] : 0.f;
+        const float t = Ot ? Ot[r * g.DTp + i] : 0.f;
+        v = __fadd_rn(__fmul_rn(v, expf(s)), t);
+      }
+      zr[g.col(j)] = v;
+    }
+    if (Os)
+      for (int i = lane; i < g.DT; i += 64) sacc += Os[r * g.DTp + i];
+    for (int c = g.DC + lane; c < g.Cp; c += 64) zr[c] = c == g.DC ? 1.f : 0.f;
+    for (int c = g.Cp + g.DT + lane; c < g.Dp; c += 64) zr[c] = 0.f;
+    sacc = wave_sum(sacc);
+    if (lane == 0) ld[r] = first ? sacc : ld[r] + sacc;
+  }
+}
+
+// Upstream gradient at z_L (stash layout), one wave per row, into natural
+// order.  Loss kinds as k_vjp2 (cnf_vjp.hip); generic: gz (+ gz_all[L-1]) and
+// gld.  Loss sums per block in fixed order: partials[block][0..2] = (loss, ce,
+// ld).
+__global__ __launch_bounds__(256) void k_wseed(const float* __restrict__ Z,
+                                               const float* __restrict__ ld,
+                                               const int64_t* __restrict__ y, int kind, float det,
+                                               float grad_scale, const float* __restrict__ gz,
+                                               const float* __restrict__ gz_last,
+                                               const float* __restrict__ gld_in,
+                                               float* __restrict__ G, float* __restrict__ gld,
+                                               float* __restrict__ partials, int64_t B, Geo g) {
+  __shared__ float red[4][3];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  const int D = g.D;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + wv; r < B; r += nw) {
+    if (kind < 0) {
+      for (int j = lane; j < D; j += 64) {
+        float v = gz ? gz[r * D + j] : 0.f;
+        if (gz_last) v += gz_last[r * D + j];
+        G[r * D + j] = v;
+      }
+      if (lane == 0) gld[r] = gld_in ? gld_in[r] : 0.f;
+      continue;
+    }
+    const float* zr = Z + r * g.Dp;
+    float m = -INFINITY;
+    for (int j = lane; j < D; j += 64) m = fmaxf(m, zr[g.col(j)]);
+    m = wave_max(m);
+    float se = 0.f;
+    for (int j = lane; j < D; j += 64) se += expf(zr[g.col(j)] - m);
+    se = wave_sum(se);
+    const float lse = m + logf(se);
+    const int64_t yy = y[r];
+    const bool ok = yy >= 0 && yy < D;
+    const int yi = ok ? (int)yy : 0;
+    const float lpy = zr[g.col(yi)] - lse;
+    const float ldr = ld[r];
+    float coef, ce, loss, gl;
+    if (kind == CNF_LOSS_CAL) {  // -(log(softmax(z)[y] + 1e-7) + ld)
+      const float py = expf(lpy);
+      ce = -logf(py + 1e-7f);
+      loss = ce - ldr;
+      coef = py / (py + 1e-7f);
+      gl = -grad_scale;
+    } else {  // CE(z, y) - det * ld
+      ce = -lpy;
+      loss = ce - det * ldr;
+      coef = 1.f;
+      gl = -det * grad_scale;
+    }
+    if (!ok) ce = loss = coef = __builtin_nanf("");
+    for (int j = lane; j < D; j += 64) {
+      const float pj = expf(zr[g.col(j)] - lse);
+      G[r * D + j] = grad_scale * coef * (pj - (j == yi ? 1.f : 0.f));
+    }
+    if (lane == 0) {
+      gld[r] = gl;
+      a0 += loss;
+      a1 += ce;
+      a2 += ldr;
+    }
+  }
+  if (kind < 0) return;
+  if (lane == 0) {
+    red[wv][0] = a0;
+    red[wv][1] = a1;
+    red[wv][2] = a2;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    float v = 0.f;
+    if (threadIdx.x < 3)
+      for (int q = 0; q < 4; ++q) v += red[q][threadIdx.x];
+    partials[blockIdx.x * 4 + threadIdx.x] = v;
+  }
+}
+
+// Back through one coupling update, one wave per row: undo the flip /
+// permutation (g_pre[fq[j]] = g_out[j]), then with e = e^{s}:
+//   G_s = g_pre_T x_T e + gld,  G_t = g_pre_T,  g_in_T = g_pre_T e,
+//   g_in_C = g_pre_C (the conditioners' share is added by the first Linear's
+//   back-prop), plus the caller's gradient of the previous layer's output.
+__global__ __launch_bounds__(256) void k_wbwd_update(
+    const float* __restrict__ gout, float* __restrict__ gin, const float* __restrict__ X,
+    const float* __restrict__ Os, const float* __restrict__ gld, float* __restrict__ Gs,
+    float* __restrict__ Gt, const float* __restrict__ gprev, const int32_t* __restrict__ fq,
+    int64_t B, Geo g) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  const int D = g.D, DT = g.DT, DTp = g.DTp;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < B; r += nw) {
+    const float gl = gld[r];
+    for (int j = lane; j < D; j += 64) {
+      const int i = fq[j];
+      const float v = gout[r * D + j];
+      float gi = v;
+      if (i < DT) {
+        const float e = Os ? expf(Os[r * DTp + i]) : 1.f;
+        if (Gs) Gs[r * DTp + i] = __fadd_rn(__fmul_rn(__fmul_rn(v, X[r * g.Dp + g.Cp + i]), e), gl);
+        if (Gt) Gt[r * DTp + i] = v;
+        gi = __fmul_rn(v, e);
+      }
+      if (gprev) gi += gprev[r * D + i];
+      gin[r * D + i] = gi;
+    }
+    for (int i = DT + lane; i < DTp; i += 64) {
+      if (Gs) Gs[r * DTp + i] = 0.f;
+      if (Gt) Gt[r * DTp + i] = 0.f;
+    }
+  }
+}
+
+inline int64_t al64(int64_t floats) { return (floats + 63) / 64 * 64; }
+
+int lin_out(const Shape& s, int k) { return k == s.n_lin - 1 ? s.DT : s.units[k + 1]; }
+int lin_in(const Shape& s, int k) { return k == 0 ? s.DC : s.units[k]; }
+int hp(const Shape& s, int k) { return r8(s.units[k + 1] + 1); }  // H_k: units + ones
+int gp(const Shape& s, int k) { return r8(lin_out(s, k)); }       // G_k
+
+Geo geo(const Shape& s) {
+  Geo g;
+  g.D = s.D;
+  g.DT = s.DT;
+  g.DC = s.DC;
+  g.Cp = r8(s.DC + 1);
+  g.DTp = r8(s.DT);
+  g.Dp = g.Cp + g.DTp;
+  return g;
+}
+
+// Workspace plan (float offsets), shared by the size query and the run.
+struct Plan {
+  int64_t stash, ld, gld, g0, g1, seed, part;
+  int64_t H[2][kMaxLin], O[2], G[2][kMaxLin];
+  int64_t total;
+  int64_t nkb, rows_kb, nseed;
+};
+
+Plan make_plan(const Shape& s, int64_t B) {
+  Plan p{};
+  const int64_t Bn = B > 0 ? B : 1;
+  const Geo g = geo(s);
+  int64_t off = 0;
+  auto take = [&](int64_t n) {
+    const int64_t o = off;
+    off += al64(n);
+    return o;
+  };
+  p.stash = take((int64_t)(s.L + 1) * Bn * g.Dp);
+  p.ld = take(Bn);
+  p.gld = take(Bn);
+  p.g0 = take(Bn * s.D);
+  p.g1 = take(Bn * s.D);
+  for (int n = 0; n < s.nets; ++n) {
+    for (int k = 0; k + 1 < s.n_lin; ++k) p.H[n][k] = take(Bn * hp(s, k));
+    p.O[n] = take(Bn * g.DTp);
+    for (int k = 0; k < s.n_lin; ++k) p.G[n][k] = take(Bn * gp(s, k));
+  }
+  p.nseed = std::min<int64_t>(1024, (Bn + 15) / 16);
+  p.seed = take(p.nseed * 4);
+  int64_t rows = (Bn + 255) / 256;
+  rows = std::max<int64_t>(256, (rows + 31) / 32 * 32);
+  p.rows_kb = rows;
+  p.nkb = (Bn + rows - 1) / rows;
+  p.part = take(p.nkb * al64(s.layer_floats));
+  p.total = off;
+  return p;
+}
+
+int64_t lin_off(const Shape& s, int k) {
+  int64_t o = 0;
+  for (int i = 0; i < k; ++i) o += (int64_t)s.units[i + 1] * s.units[i] + s.units[i + 1];
+  return o;
+}
+
+int check_launch() {
+  hipError_t err = hipGetLastError();
+  if (err != hipSuccess) {
+    set_hip_error(err);
+    return CNF_ERR_HIP;
+  }
+  return CNF_OK;
+}
+
+int gemm_nc(int cols) { return std::min(kBN / 32, (cols + 31) / 32); }
+
+size_t gemm_lds(int cols, int K, bool pair) {
+  return (size_t)((K + 7) & ~7) * (32 * gemm_nc(cols) + 8) * 4 * (pair ? 2 : 1);
+}
+
+template <int NC>
+void launch_nc(bool bt, int epi, bool pair, dim3 grid, size_t lds, hipStream_t st,
+               const GemmArgs& ga) {
+  if (bt && epi == kEpiBias)
+    hipLaunchKernelGGL((k_wgemm<true, kEpiBias, false, NC>), grid, dim3(256), lds, st, ga);
+  else if (bt && epi == kEpiBiasRelu)
+    hipLaunchKernelGGL((k_wgemm<true, kEpiBiasRelu, false, NC>), grid, dim3(256), lds, st, ga);
+  else if (!bt && epi == kEpiMask)
+    hipLaunchKernelGGL((k_wgemm<false, kEpiMask, false, NC>), grid, dim3(256), lds, st, ga);
+  else if (!bt && epi == kEpiAdd && pair)
+    hipLaunchKernelGGL((k_wgemm<false, kEpiAdd, true, NC>), grid, dim3(256), lds, st, ga);
+  else
+    hipLaunchKernelGGL((k_wgemm<false, kEpiAdd, false, NC>), grid, dim3(256), lds, st, ga);
+}
+
+// One GEMM launch over B rows; cols = columns written (N plus pad).
+void gemm(const GemmArgs& ga, int64_t B, int cols, int K, int nz, bool bt, int epi, bool pair,
+          hipStream_t st) {
+  const unsigned ny = (unsigned)((cols + kBN - 1) / kBN);
+  const size_t lds = gemm_lds(cols, K, pair);
+  const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(4, 160 * 1024 / lds));
+  const int64_t want = std::max<int64_t>(1, (int64_t)256 * per_cu / (ny * nz));
+  const unsigned nx = (unsigned)std::min<int64_t>(want, ((B + 31) / 32 + 3) / 4);
+  const dim3 grid(nx, ny, (unsigned)nz);
+  switch (gemm_nc(cols)) {
+    case 1: launch_nc<1>(bt, epi, pair, grid, lds, st, ga); break;
+    case 2: launch_nc<2>(bt, epi, pair, grid, lds, st, ga); break;
+    default: launch_nc<2>(bt, epi, pair, grid, lds, st, ga); break;
+  }
+}
+
+}  // namespace
+
+// Every Linear's weight slice (K x 32*NC floats, both nets for the paired
+// launch) must fit one CU's LDS: widths up to ~290 (CNF_MAX_WIDTH 512 shapes
+// beyond that keep the torch fallback).
+bool wvjp_ok(const Shape& s) {
+  if (s.family != Family::kTile || s.strict) return false;
+  constexpr size_t kLds = 160 * 1024;
+  for (int k = 0; k < s.n_lin; ++k) {
+    const int cols = k == s.n_lin - 1 ? s.DT : hp(s, k);
+    if (gemm_lds(cols, lin_in(s, k), false) > kLds) return false;               // forward
+    if (k > 0 && gemm_lds(gp(s, k - 1), lin_out(s, k), false) > kLds) return false;  // back-prop
+  }
+  return gemm_lds(s.DC, lin_out(s, 0), s.nets == 2) <= kLds;
+}
+
+int wvjp_workspace(const Shape& s, int64_t B, size_t* bytes) {
+  if (!wvjp_ok(s)) return CNF_ERR_UNSUPPORTED;
+  *bytes = (size_t)make_plan(s, B).total * 4;
+  return CNF_OK;
+}
+
+int wvjp_run(const Shape& s, const void* prepared, const float* x, const int64_t* y,
+             const float* gz, const float* gz_all, const float* gld_in, int kind, float det,
+             float grad_scale, float* loss_terms, float* grads, float* dx, int64_t B, void* ws,
+             size_t ws_bytes, hipStream_t st) {
+  if (!wvjp_ok(s)) return CNF_ERR_UNSUPPORTED;
+  const Plan p = make_plan(s, B);
+  if (!ws || ws_bytes < (size_t)p.total * 4) return CNF_ERR_NULL;
+  const int64_t P = s.layer_floats * s.L;
+  if (B == 0) {
+    if (P > 0 && hipMemsetAsync(grads, 0, (size_t)P * 4, st) != hipSuccess) return check_launch();
+    if (loss_terms && hipMemsetAsync(loss_terms, 0, 3 * 4, st) != hipSuccess) return check_launch();
+    return check_launch();
+  }
+  float* W = static_cast<float*>(ws);
+  const char* base = static_cast<const char*>(prepared);
+  const int32_t* fq = reinterpret_cast<const int32_t*>(base);
+  const float* plain = reinterpret_cast<const float*>(base + idx_bytes(s)) + s.plain_region;
+  const Geo geom = geo(s);
+  const int D = s.D, DT = s.DT, DC = s.DC, NL = s.n_lin, L = s.L;
+  const int64_t PL = s.layer_floats, PS = al64(PL), Dp = geom.Dp;
+  float* ld = W + p.ld;
+  float* gld = W + p.gld;
+  float* part = W + p.part;
+  auto Xs = [&](int l) { return W + p.stash + (int64_t)l * B * Dp; };  // input of layer l
+  auto wptr = [&](int l, int n, int k) { return plain + l * PL + n * s.net_floats + lin_off(s, k); };
+  auto bptr = [&](int l, int n, int k) {
+    return wptr(l, n, k) + (int64_t)s.units[k + 1] * s.units[k];
+  };
+  const unsigned wave_blocks = (unsigned)std::min<int64_t>((B + 3) / 4, 16384);
+
+  // conditioner forward of layer l from its stashed input: H[n][k], O[n]
+  auto nets_forward = [&](int l) {
+    for (int k = 0; k < NL; ++k) {
+      GemmArgs ga{};
+      ga.M = B;
+      const bool last = k == NL - 1;
+      for (int n = 0; n < s.nets; ++n) {
+        GemmJob& j = ga.job[n];
+        j.A = k == 0 ? Xs(l) : W + p.H[n][k - 1];
+        j.lda = k == 0 ? Dp : hp(s, k - 1);
+        j.K = lin_in(s, k);
+        j.Bw = wptr(l, n, k) + (k == 0 ? DT : 0);
+        j.ldb = s.units[k];
+        j.N = lin_out(s, k);
+        j.bias = bptr(l, n, k);
+        j.C = last ? W + p.O[n] : W + p.H[n][k];
+        j.ldc = last ? geom.DTp : hp(s, k);
+        j.ldw = last ? j.N : hp(s, k);
+        j.ones = !last;
+      }
+      gemm(ga, B, ga.job[0].ldw, lin_in(s, k), s.nets, true, last ? kEpiBias : kEpiBiasRelu,
+           false, st);
+    }
+  };
+  const float* Os = s.scale ? W + p.O[0] : nullptr;
+  const float* Ot = s.shift ? W + p.O[s.scale] : nullptr;
+
+  // ---- forward sweep ----
+  hipLaunchKernelGGL(k_wstash, dim3(wave_blocks), dim3(256), 0, st, x, Xs(0), B, geom);
+  for (int l = 0; l < L; ++l) {
+    if (s.nets) nets_forward(l);
+    hipLaunchKernelGGL(k_wfwd_update, dim3(wave_blocks), dim3(256), 0, st, Xs(l), Xs(l + 1), ld,
+                       Os, Ot, fq + l * D, B, geom, l == 0);
+  }
+  // ---- seed ----
+  float* g[2] = {W + p.g0, W + p.g1};
+  int cur = 0;
+  hipLaunchKernelGGL(k_wseed, dim3((unsigned)p.nseed), dim3(256), 0, st, Xs(L), ld, y, kind, det,
+                     grad_scale, gz, gz_all ? gz_all + (int64_t)(L - 1) * B * D : nullptr, gld_in,
+                     g[0], gld, W + p.seed, B, geom);
+  if (kind >= 0) reduce_partials(W + p.seed, (int)p.nseed, 4, 0, nullptr, loss_terms, st);
+  if (P > 0 && hipMemsetAsync(part, 0, (size_t)p.nkb * PS * 4, st) != hipSuccess)
+    return check_launch();
+
+  // ---- backward sweep ----
+  for (int l = L - 1; l >= 0; --l) {
+    if (s.nets) nets_forward(l);
+    float* gin = (l == 0 && dx) ? dx : g[cur ^ 1];
+    float* Gs = s.scale ? W + p.G[0][NL - 1] : nullptr;
+    float* Gt = s.shift ? W + p.G[s.scale][NL - 1] : nullptr;
+    hipLaunchKernelGGL(k_wbwd_update, dim3(wave_blocks), dim3(256), 0, st, g[cur], gin, Xs(l), Os,
+                       gld, Gs, Gt, gz_all && l > 0 ? gz_all + (int64_t)(l - 1) * B * D : nullptr,
+                       fq + l * D, B, geom);
+    if (s.nets == 0) {
+      cur ^= 1;
+      continue;
+    }
+    for (int k = NL - 1; k >= 1; --k) {  // G_{k-1} = (G_k W_k) * relu'(H_{k-1})
+      GemmArgs ga{};
+      ga.M = B;
+      for (int n = 0; n < s.nets; ++n) {
+        GemmJob& j = ga.job[n];
+        j.A = W + p.G[n][k];
+        j.lda = gp(s, k);
+        j.K = lin_out(s, k);
+        j.Bw = wptr(l, n, k);
+        j.ldb = s.units[k];
+        j.N = s.units[k];
+        j.C = W + p.G[n][k - 1];
+        j.ldc = gp(s, k - 1);
+        j.ldw = gp(s, k - 1);
+        j.mask = W + p.H[n][k - 1];
+        j.ldm = hp(s, k - 1);
+      }
+      gemm(ga, B, gp(s, k - 1), lin_out(s, k), s.nets, false, kEpiMask, false, st);
+    }
+    {  // g_in[:, DT:] += sum over nets of G_0 W_0[:, DT:]
+      GemmArgs ga{};
+      ga.M = B;
+      GemmJob& j = ga.job[0];
+      j.A = W + p.G[0][0];
+      j.lda = gp(s, 0);
+      j.K = lin_out(s, 0);
+      j.Bw = wptr(l, 0, 0) + DT;
+      j.ldb = D;
+      if (s.nets == 2) {
+        j.A2 = W + p.G[1][0];
+        j.lda2 = j.lda;
+        j.Bw2 = wptr(l, 1, 0) + DT;
+        j.ldb2 = D;
+      }
+      j.N = DC;
+      j.C = gin + DT;
+      j.ldc = D;
+      j.ldw = DC;
+      gemm(ga, B, DC, j.K, 1, false, kEpiAdd, s.nets == 2, st);
+    }
+    // weight / bias gradients of every Linear of both nets: one launch
+    DwArgs da{};
+    da.partials = part;
+    da.M = B;
+    da.rows = p.rows_kb;
+    da.PS = PS;
+    int jobs = 0, max_subs = 1;
+    for (int n = 0; n < s.nets; ++n) {
+      for (int k = 0; k < NL; ++k) {
+        DwJob& j = da.job[jobs++];
+        j.G = W + p.G[n][k];
+        j.ldg = gp(s, k);
+        j.H = k == 0 ? Xs(l) : W + p.H[n][k - 1];
+        j.ldh = k == 0 ? Dp : hp(s, k - 1);
+        j.N = lin_out(s, k);
+        j.K = lin_in(s, k);
+        j.woff = n * s.net_floats + lin_off(s, k) + (k == 0 ? DT : 0);
+        j.wld = s.units[k];
+        j.boff = n * s.net_floats + lin_off(s, k) + (int64_t)s.units[k + 1] * s.units[k];
+        j.tiles_k = (j.K + 1 + kDwCols - 1) / kDwCols;
+        max_subs = std::max(max_subs, j.tiles_k * ((j.N + 31) / 32));
+      }
+    }
+    hipLaunchKernelGGL(k_wdw<kDwCols / 32>,
+                       dim3((unsigned)p.nkb, (unsigned)jobs, (unsigned)max_subs), dim3(64), 0, st,
+                       da);
+    reduce_partials(part, (int)p.nkb, (int)PS, (int)PL, grads + (int64_t)l * PL, nullptr, st);
+    cur ^= 1;
+  }
+  return check_launch();
+}
+
+}  // namespace cnf
