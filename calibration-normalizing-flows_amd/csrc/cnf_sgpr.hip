@@ -2,8 +2,11 @@
 // every conditioner Linear fits 32 floats (W[nout][nin] + b[nout]: the
 // reference default D=10, hidden_size=[5,5], flows/flows.py:71, is three 5x5
 // Linears per net).  Serves every final-output launch of those shapes:
-// forward (+log-det), inverse, the fused calibrator eval loss, the fused
-// predict pass, and every-layer outputs (the reference's zs / xs lists).
+// forward (+log-det), inverse, the fused calibrator eval loss and the fused
+// predict pass.
+//
+// (Every-layer outputs, the reference's zs / xs lists, are served by k_valu:
+// its LDS-staged stores are faster for the L*B*D floats.)
 //
 // Reference semantics restated (paths in the reference repo):
 //   MLP.forward                 flows/utils.py:26-31
@@ -542,25 +545,26 @@ struct KV {
   int tr;
 };
 
-// variants without permutation: fwd, inv, loss, predict, fwd+all, inv+all;
-// with a random_flip permutation: fwd, inv, fwd+all, inv+all
-enum Var { vFwd, vInv, vLoss, vPredict, vFwdAll, vInvAll, kNVar };
+// variants without permutation: fwd, inv, loss, predict; with a random_flip
+// permutation: fwd, inv.  The every-layer-output form (ALL) is not
+// instantiated: those launches go to k_valu, whose LDS-staged stores write
+// the L*B*D floats faster (cnf_valu.hip valu_run); ALL stays as a template
+// switch for A/B builds.
+enum Var { vFwd, vInv, vLoss, vPredict, kNVar };
 
 struct SEntry {
   int D, H1, H2;
   KV fn[2][kNVar];  // [nets - 1][variant]
-  KV pfn[2][4];     // [nets - 1][fwd, inv, fwd+all, inv+all] with permutation
+  KV pfn[2][2];     // [nets - 1][fwd, inv] with permutation
 };
 
 #define CNF_K(D, H1, H2, N, M, A, P) \
   {k_sgpr<D, H1, H2, N, M, A, P>, 128 * pairs_per_lane<A, P>()}
 #define CNF_SV(D, H1, H2, N)                                                                  \
   {CNF_K(D, H1, H2, N, kFwd, false, false), CNF_K(D, H1, H2, N, kInv, false, false),           \
-   CNF_K(D, H1, H2, N, kLoss, false, false), CNF_K(D, H1, H2, N, kPredict, false, false),      \
-   CNF_K(D, H1, H2, N, kFwd, true, false), CNF_K(D, H1, H2, N, kInv, true, false)}
+   CNF_K(D, H1, H2, N, kLoss, false, false), CNF_K(D, H1, H2, N, kPredict, false, false)}
 #define CNF_SP(D, H1, H2, N)                                                                  \
-  {CNF_K(D, H1, H2, N, kFwd, false, true), CNF_K(D, H1, H2, N, kInv, false, true),             \
-   CNF_K(D, H1, H2, N, kFwd, true, true), CNF_K(D, H1, H2, N, kInv, true, true)}
+  {CNF_K(D, H1, H2, N, kFwd, false, true), CNF_K(D, H1, H2, N, kInv, false, true)}
 #define CNF_SGPR(D, H1, H2) \
   {D, H1, H2, {CNF_SV(D, H1, H2, 1), CNF_SV(D, H1, H2, 2)}, {CNF_SP(D, H1, H2, 1), CNF_SP(D, H1, H2, 2)}}
 
@@ -606,11 +610,11 @@ int resident_blocks(const KV& k, size_t lds) {
 
 const KV* pick(const SEntry* e, const Shape& s, int mode, bool all) {
   const int n = s.scale ? 1 : 0;
+  if (all) return nullptr;  // k_valu serves every-layer outputs
   if (s.any_perm) {
     if (mode == kLoss || mode == kPredict) return nullptr;  // k_valu handles these
-    return &e->pfn[n][(mode == kInv ? 1 : 0) + (all ? 2 : 0)];
+    return &e->pfn[n][mode == kInv ? 1 : 0];
   }
-  if (all) return &e->fn[n][mode == kInv ? vInvAll : vFwdAll];
   return &e->fn[n][mode];
 }
 

@@ -226,87 +226,6 @@ __device__ __forceinline__ void block_sum3(float a, float b, float c, float* sm,
   }
 }
 
-// One-launch form for persistent grids (each block finishes once): after its
-// partial, thread 0 takes a device-scope ticket; the block that draws the last
-// one adds every partial in block order and writes terms[0..2], then resets
-// the ticket.  Hand-off (cdna_hip_programming.md Guideline 16, write-through
-// form): partials stored sc1 and drained by vmcnt(0) before a relaxed agent
-// ticket add; the last arriver reads them with sc1 loads.  No release fence
-// (it would write back the XCD's whole L2 -- every freshly stored z line).
-template <int ROWS>
-__device__ __forceinline__ void block_sum3_last(float a, float b, float c, float* sm, float* part,
-                                                unsigned* ticket, float* terms, int nblk) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    a += __shfl_xor(a, off);
-    b += __shfl_xor(b, off);
-    c += __shfl_xor(c, off);
-  }
-  const int tid = threadIdx.x, w = tid >> 6;
-  lds_barrier();
-  if ((tid & 63) == 0) {
-    sm[4 * w] = a;
-    sm[4 * w + 1] = b;
-    sm[4 * w + 2] = c;
-  }
-  lds_barrier();
-  if (tid == 0) {
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
-    for (int i = 0; i < ROWS / 64; ++i) {
-      s0 += sm[4 * i];
-      s1 += sm[4 * i + 1];
-      s2 += sm[4 * i + 2];
-    }
-    float* dst = part + (int64_t)blockIdx.x * 4;
-    __hip_atomic_store(dst, s0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(dst + 1, s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(dst + 2, s2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT);
-    sm[64] = t == (unsigned)(nblk - 1) ? 1.f : 0.f;
-  }
-  lds_barrier();
-  if (sm[64] == 0.f) return;  // block-uniform
-  // every partial of this thread's stride in flight at once (<= 8 per thread)
-  constexpr int KMAX = 8;
-  float r[3] = {0.f, 0.f, 0.f};
-  for (int b0 = tid; b0 < nblk; b0 += KMAX * ROWS) {
-    float v[KMAX][3];
-#pragma unroll
-    for (int k = 0; k < KMAX; ++k) {
-      const int bb = b0 + k * ROWS;
-#pragma unroll
-      for (int e = 0; e < 3; ++e)
-        v[k][e] = bb < nblk ? __hip_atomic_load(part + (int64_t)bb * 4 + e, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT)
-                            : 0.f;
-    }
-#pragma unroll
-    for (int k = 0; k < KMAX; ++k)
-#pragma unroll
-      for (int e = 0; e < 3; ++e) r[e] += v[k][e];
-  }
-  lds_barrier();
-  sm[tid] = r[0];
-  sm[ROWS + tid] = r[1];
-  sm[2 * ROWS + tid] = r[2];
-  lds_barrier();
-  for (int h = ROWS / 2; h >= 1; h >>= 1) {
-    if (tid < h) {
-      sm[tid] += sm[tid + h];
-      sm[ROWS + tid] += sm[ROWS + tid + h];
-      sm[2 * ROWS + tid] += sm[2 * ROWS + tid + h];
-    }
-    lds_barrier();
-  }
-  if (tid == 0) {
-    terms[0] = sm[0];
-    terms[1] = sm[ROWS];
-    terms[2] = sm[2 * ROWS];
-    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
 
 template <int ROWS>
 __device__ __forceinline__ void store_ld(float* ld_out, int64_t row0, int tid, int nrows, float v) {

@@ -111,11 +111,9 @@ int cnf_inverse(const cnf_desc* desc, const void* prepared, const float* z, floa
  * calibrators.py:297-317; the per-step NLL of a sharded batch):
  *   loss_terms[3]  {sum of per-row loss, sum of ce, sum of ld} over the B rows
  *   z, logdet      as cnf_forward, each may be NULL
- * The fused pass writes per-block partial sums into the workspace; they are
- * added in block order (deterministic) either by the block that finishes last
- * (persistent grid: one launch) or by a one-block follow-up launch.  The
- * workspace must be zero-filled before its first use; every call leaves it
- * reusable.  Narrow flows only (valu-fused). */
+ * The fused pass writes per-block partial sums into the workspace (no
+ * initialisation needed); a one-block follow-up launch adds them in block
+ * order (deterministic).  Narrow flows only (sgpr-fused / valu-fused). */
 int cnf_forward_loss_workspace_bytes(const cnf_desc* desc, int64_t B, size_t* bytes);
 int cnf_forward_loss(const cnf_desc* desc, const void* prepared, const float* x,
                      const int64_t* y, int32_t loss_kind, float det, float* z, float* logdet,

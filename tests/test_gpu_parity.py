@@ -294,14 +294,19 @@ def test_valu_family_matches_reference_fixture(name):
 
 def test_every_layer_outputs_at_full_size():
     """The zs list (every layer's z, 284 B/row) at 2^20 rows with random_flip:
-    its last entry is bitwise the final-only output, log-dets agree."""
+    its last entry agrees with the final-only output and the log-dets agree
+    (different kernels: k_valu stores every layer, k_sgpr serves final-only
+    launches with exp2 of log2(e)-scaled weights, so agreement is to fp32
+    rounding, not bitwise)."""
     flow = _make_flow(10, 6, [5, 5], 0.1, 5, random_flip=True)
     x = _logits((1 << 20) + 33, 10, 7)
     with torch.no_grad():
         zs, ld = flow(x)
         z, ld2 = flow.transform(x)
         xs, ild = flow.backward(z)
-    assert len(zs) == 6 and torch.equal(zs[-1], z) and torch.equal(ld, ld2)
+    assert len(zs) == 6
+    assert ((zs[-1] - z).abs() / (z.abs() + 1)).max().item() <= TOL
+    assert ((ld - ld2).abs() / (ld2.abs() + 1)).max().item() <= TOL
     assert ((xs[-1] - x).abs() / (x.abs() + 1)).max().item() <= TOL
     assert ((ild + ld).abs() / (ld.abs() + 1)).max().item() <= TOL
     idx = torch.randperm(x.shape[0], generator=torch.Generator().manual_seed(2))[:1024].to(DEV)
