@@ -90,9 +90,12 @@ constexpr int kWaves = 4;  // waves per block
 template <bool ALL, bool PERM>
 constexpr int pairs_per_lane() { return (ALL || PERM) ? 1 : CNF_SGPR_PAIRS; }
 // register budget (resident waves per SIMD) for a lane of P pairs
+#ifndef CNF_SGPR_WPS  // A/B builds: -DCNF_SGPR_WPS=n for the unpermuted one-pair variants
+#define CNF_SGPR_WPS 5
+#endif
 template <int MODE, bool ALL, bool PERM>
 constexpr int waves_per_simd() {
-  return pairs_per_lane<ALL, PERM>() == 2 ? 4 : (PERM ? 4 : 5);
+  return pairs_per_lane<ALL, PERM>() == 2 ? 4 : (PERM ? 4 : CNF_SGPR_WPS);
 }
 
 enum Mode { kFwd = 0, kInv = 1, kLoss = 2, kPredict = 3 };

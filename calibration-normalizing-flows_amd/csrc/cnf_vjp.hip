@@ -434,28 +434,38 @@ __global__ __launch_bounds__(kVRows) void k_vjp(
 // Many entries (weight gradients): a block owns 64 consecutive entries and
 // its 4 waves split the blocks b = g, g+4, ... (coalesced 256-B rows); the 4
 // group sums are then added in group order.
+// Column sums of per-block partial records: block (x, y) adds rows
+// [y*R, min(nblk, (y+1)*R)) of columns [64x, 64x + 64) -- four row groups of
+// 64 lanes, four loads in flight each -- and writes the sums to out + y*ostride
+// (ostride = R*PS: in place over the chunk's first row, which only this block
+// reads).  grid.y = 1 gives the final sums.  Fixed grouping: deterministic.
 __global__ __launch_bounds__(256) void k_reduce_cols(const float* __restrict__ partials, int nblk,
-                                                     int PS, int NE, float* __restrict__ out) {
+                                                     int PS, int NE, float* __restrict__ out,
+                                                     int R, int64_t ostride) {
   __shared__ float red[256];
   const int e = blockIdx.x * 64 + (threadIdx.x & 63), g = threadIdx.x >> 6;
+  const int r0 = (int)blockIdx.y * R, n = min(R, nblk - r0);
+  const float* base = partials + (int64_t)r0 * PS;
   float s = 0.f;
   if (e < NE) {
     int b = g;
-    for (; b + 12 < nblk; b += 16) {
-      const float a0 = partials[(int64_t)b * PS + e], a1 = partials[(int64_t)(b + 4) * PS + e];
-      const float a2 = partials[(int64_t)(b + 8) * PS + e];
-      const float a3 = partials[(int64_t)(b + 12) * PS + e];
+    for (; b + 12 < n; b += 16) {
+      const float a0 = base[(int64_t)b * PS + e], a1 = base[(int64_t)(b + 4) * PS + e];
+      const float a2 = base[(int64_t)(b + 8) * PS + e];
+      const float a3 = base[(int64_t)(b + 12) * PS + e];
       s += a0;
       s += a1;
       s += a2;
       s += a3;
     }
-    for (; b < nblk; b += 4) s += partials[(int64_t)b * PS + e];
+    for (; b < n; b += 4) s += base[(int64_t)b * PS + e];
   }
   red[threadIdx.x] = s;
   __syncthreads();
-  if (g == 0 && e < NE) out[e] = ((red[threadIdx.x] + red[threadIdx.x + 64]) +
-                                  red[threadIdx.x + 128]) + red[threadIdx.x + 192];
+  if (g == 0 && e < NE)
+    out[(int64_t)blockIdx.y * ostride + e] =
+        ((red[threadIdx.x] + red[threadIdx.x + 64]) + red[threadIdx.x + 128]) +
+        red[threadIdx.x + 192];
 }
 
 // The 3 loss sums: ONE wave.  Lane l adds blocks l, l+64, ... in order (eight
@@ -1218,9 +1228,24 @@ int64_t grid_v2(const Shape& s, VFn2 fn, int64_t B) {
 
 int reduce_partials(const float* partials, int nblk, int PS, int P, float* grads, float* terms,
                     hipStream_t st) {
-  if (P > 0)
-    hipLaunchKernelGGL(k_reduce_cols, dim3((unsigned)((P + 63) / 64)), dim3(256), 0, st,
-                       partials, nblk, PS, P, grads);
+  if (P > 0) {
+    // many records: a first pass folds chunks of R records into each chunk's
+    // first record (in place), so enough blocks share the read; then the
+    // chunk sums are added in order
+    const unsigned cols = (unsigned)((P + 63) / 64);
+    int nrec = nblk, stride = PS;
+    if (nblk >= 128) {
+      const int S = std::min(64, nblk / 32), R = (nblk + S - 1) / S;
+      const int S2 = (nblk + R - 1) / R;
+      float* part = const_cast<float*>(partials);
+      hipLaunchKernelGGL(k_reduce_cols, dim3(cols, (unsigned)S2), dim3(256), 0, st, partials, nblk,
+                         PS, P, part, R, (int64_t)R * PS);
+      nrec = S2;
+      stride = R * PS;
+    }
+    hipLaunchKernelGGL(k_reduce_cols, dim3(cols, 1), dim3(256), 0, st, partials, nrec, stride, P,
+                       grads, nrec, (int64_t)0);
+  }
   const bool r4 = PS == 4 && P == 0 && (reinterpret_cast<uintptr_t>(partials) & 15) == 0;
   if (terms && r4)
     hipLaunchKernelGGL(k_reduce_rows4, dim3(1), dim3(kRR), 0, st,
