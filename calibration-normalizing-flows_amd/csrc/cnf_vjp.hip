@@ -210,7 +210,7 @@ __global__ __launch_bounds__(kVRows) void k_vjp(
 
     // ---- forward sweep (stash the transformed inputs) --------------------
     float ld = 0.f;
-    auto fwd = [&](auto O_, int l) {
+    auto fwd = [&](auto O_, int l) __attribute__((always_inline)) {
       constexpr bool O = decltype(O_)::value;
 #pragma unroll
       for (int j = 0; j < DT; ++j) stash[(l * DT + j) * kVRows + lane] = v[R<D, O>(j)];
@@ -229,7 +229,7 @@ __global__ __launch_bounds__(kVRows) void k_vjp(
     // ---- upstream gradient at z_L (orientation OL = L & 1) ---------------
     float g[D];
     float gld = 0.f;
-    auto seed = [&](auto O_) {
+    auto seed = [&](auto O_) __attribute__((always_inline)) {
       constexpr bool O = decltype(O_)::value;
       if constexpr (LOSS) {
         float z[D];
@@ -289,7 +289,7 @@ __global__ __launch_bounds__(kVRows) void k_vjp(
     else seed(std::false_type{});
 
     // ---- backward sweep ---------------------------------------------------
-    auto bwd = [&](auto Oc_, int l) {
+    auto bwd = [&](auto Oc_, int l) __attribute__((always_inline)) {
       constexpr bool Oc = decltype(Oc_)::value;  // orientation of z_l
       constexpr bool Oi = !Oc;
       if (gz_all && valid) {
@@ -576,6 +576,14 @@ __global__ __launch_bounds__(kRR) void k_reduce_rows4(const float4* __restrict__
 //             wave's whole run and are written once, as this wave's partial.
 // Partials are summed in wave order by k_reduce_cols (deterministic).
 // ===========================================================================
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
 constexpr int kV2TR = 128;   // rows per wave tile (lane l: rows 2l, 2l+1)
 constexpr int kV2LMax = 8;   // layers the register accumulators hold
 constexpr int kV2SS = 68;    // stage row stride in floats (64 rows + pad, 16-B aligned)
@@ -855,7 +863,7 @@ __global__ __launch_bounds__(64, 2) void k_vjp2(const float* __restrict__ W,
 
     // ---- forward sweep (plain weights, nothing stashed) ----
     f2 ld = zero;
-    auto fwd = [&](auto O_, int l) {
+    auto fwd = [&](auto O_, int l) __attribute__((always_inline)) {
       constexpr bool O = decltype(O_)::value;
       const float* wl = W + (int64_t)l * LF;
       f2 c[DC];
@@ -897,7 +905,7 @@ __global__ __launch_bounds__(64, 2) void k_vjp2(const float* __restrict__ W,
     // ---- upstream gradient at z_L (orientation L & 1) ----
     f2 g[D];
     f2 gld = zero;
-    auto seed = [&](auto O_) {
+    auto seed = [&](auto O_) __attribute__((always_inline)) {
       constexpr bool O = decltype(O_)::value;
       if constexpr (LOSS) {
 #pragma unroll
@@ -959,8 +967,12 @@ __global__ __launch_bounds__(64, 2) void k_vjp2(const float* __restrict__ W,
     else seed(std::false_type{});
 
     // ---- backward sweep ----
-    auto bwd = [&](auto Oc_, int l) {
-      constexpr bool Oc = decltype(Oc_)::value;  // orientation of z_l
+    // layer index compile-time (static_for below): the per-layer gradient
+    // accumulators acc[l][net] stay in registers (a runtime-indexed select
+    // over them was lowered to scratch)
+    auto bwd = [&](auto LI) __attribute__((always_inline)) {
+      constexpr int l = decltype(LI)::value;
+      constexpr bool Oc = ((l + 1) & 1) != 0;  // orientation of z_l
       constexpr bool Oi = !Oc;
       if (a.gz_all) {
 #pragma unroll
@@ -1015,14 +1027,7 @@ __global__ __launch_bounds__(64, 2) void k_vjp2(const float* __restrict__ W,
         for (int m = 0; m < H1; ++m) H[DC + m] = sh1[m];
 #pragma unroll
         for (int m = 0; m < H2; ++m) H[DC + H1 + m] = sh2[m];
-        floatx4 tmp = wgrad_tile<GS, HS>(st, G, H, lane, floatx4{0.f, 0.f, 0.f, 0.f});
-        switch (l) {
-#define CNF_V2ACC(i) \
-  case i: acc[i][0] += tmp; break;
-          CNF_V2ACC(0) CNF_V2ACC(1) CNF_V2ACC(2) CNF_V2ACC(3)
-          CNF_V2ACC(4) CNF_V2ACC(5) CNF_V2ACC(6) CNF_V2ACC(7)
-#undef CNF_V2ACC
-        }
+        acc[l][0] = wgrad_tile<GS, HS>(st, G, H, lane, acc[l][0]);
       }
       {  // t-net: d/dt = g_T (before the e^s scaling of the s-net branch)
         f2 G[GS];
@@ -1036,15 +1041,7 @@ __global__ __launch_bounds__(64, 2) void k_vjp2(const float* __restrict__ W,
         for (int m = 0; m < H1; ++m) H[DC + m] = th1[m];
 #pragma unroll
         for (int m = 0; m < H2; ++m) H[DC + H1 + m] = th2[m];
-        floatx4 tmp = wgrad_tile<GS, HS>(st, G, H, lane, floatx4{0.f, 0.f, 0.f, 0.f});
-        constexpr int nt = NETS - 1;
-        switch (l) {
-#define CNF_V2ACC(i) \
-  case i: acc[i][nt] += tmp; break;
-          CNF_V2ACC(0) CNF_V2ACC(1) CNF_V2ACC(2) CNF_V2ACC(3)
-          CNF_V2ACC(4) CNF_V2ACC(5) CNF_V2ACC(6) CNF_V2ACC(7)
-#undef CNF_V2ACC
-        }
+        acc[l][NETS - 1] = wgrad_tile<GS, HS>(st, G, H, lane, acc[l][NETS - 1]);
       }
 #pragma unroll
       for (int j = 0; j < DT; ++j) {
@@ -1054,15 +1051,10 @@ __global__ __launch_bounds__(64, 2) void k_vjp2(const float* __restrict__ W,
 #pragma unroll
       for (int k = 0; k < DC; ++k) g[R<D, Oi>(DT + k)] += gc[k];
     };
-    int lb = L - 1;
-    if ((lb & 1) == 0) {  // layer L-1 even: its output orientation is 1
-      bwd(std::true_type{}, lb);
-      --lb;
-    }
-    for (; lb >= 1; lb -= 2) {
-      bwd(std::false_type{}, lb);
-      bwd(std::true_type{}, lb - 1);
-    }
+    static_for<0, kV2LMax>([&](auto I) __attribute__((always_inline)) {
+      constexpr int l = kV2LMax - 1 - decltype(I)::value;
+      if (l < L) bwd(std::integral_constant<int, l>{});
+    });
     if (a.dx) {
 #pragma unroll
       for (int j = 0; j < D; ++j) {
@@ -1085,17 +1077,12 @@ __global__ __launch_bounds__(64, 2) void k_vjp2(const float* __restrict__ W,
   }
   // the lane's accumulator cells: C[i = 4 (lane/16) + e][j = lane % 16]
   const int j = lane & 15, i0 = 4 * (lane >> 4);
-  for (int l = 0; l < L && l < kV2LMax; ++l) {
+  static_for<0, kV2LMax>([&](auto I) __attribute__((always_inline)) {
+    constexpr int l = decltype(I)::value;
+    if (l >= L) return;
 #pragma unroll
     for (int n = 0; n < NETS; ++n) {
-      floatx4 c4 = floatx4{0.f, 0.f, 0.f, 0.f};
-      switch (l) {
-#define CNF_V2GET(q) \
-  case q: c4 = acc[q][n]; break;
-        CNF_V2GET(0) CNF_V2GET(1) CNF_V2GET(2) CNF_V2GET(3)
-        CNF_V2GET(4) CNF_V2GET(5) CNF_V2GET(6) CNF_V2GET(7)
-#undef CNF_V2GET
-      }
+      const floatx4 c4 = acc[l][n];
       // net n's parameters follow the layer's state_dict order: s-net first
       const int base = l * NETS * NFN + n * NFN;
 #pragma unroll
@@ -1104,7 +1091,7 @@ __global__ __launch_bounds__(64, 2) void k_vjp2(const float* __restrict__ W,
         if (q >= 0) out[base + q] = c4[e];
       }
     }
-  }
+  });
   if constexpr (LOSS) {
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
@@ -1135,10 +1122,14 @@ struct VEntry {
    VS<D, H1, H2>::HS, VS<D, H1, H2>::TG, VS<D, H1, H2>::TH, VS<D, H1, H2>::ACC}
 
 const VEntry kVTable[] = {
+#ifdef CNF_VJP_DEV  // development builds: the headline shape only
+    CNF_VJP(10, 5, 5),
+#else
     CNF_VJP(2, 5, 5), CNF_VJP(3, 5, 5), CNF_VJP(4, 5, 5), CNF_VJP(5, 5, 5), CNF_VJP(6, 5, 5),
     CNF_VJP(8, 5, 5), CNF_VJP(10, 5, 5), CNF_VJP(3, 3, 3), CNF_VJP(8, 3, 3), CNF_VJP(10, 3, 3),
     CNF_VJP(3, 3, 0), CNF_VJP(10, 10, 0), CNF_VJP(10, 10, 10), CNF_VJP(3, 0, 0),
     CNF_VJP(10, 0, 0), CNF_VJP(10, 7, 0), CNF_VJP(10, 5, 0), CNF_VJP(3, 5, 0),
+#endif
 };
 
 const VEntry* find_entry(const Shape& s) {
@@ -1175,11 +1166,15 @@ struct V2Entry {
 
 // the packed-SGPR shapes (cnf_sgpr.hip's table): every one has GS, HS <= 16
 const V2Entry kV2Table[] = {
+#ifdef CNF_VJP_DEV
+    CNF_V2(10, 5, 5),
+#else
     CNF_V2(2, 5, 5), CNF_V2(3, 5, 5), CNF_V2(4, 5, 5), CNF_V2(5, 5, 5),
     CNF_V2(6, 5, 5), CNF_V2(8, 5, 5), CNF_V2(10, 5, 5),
     CNF_V2(3, 3, 3), CNF_V2(8, 3, 3), CNF_V2(10, 3, 3),
     CNF_V2(3, 3, 0), CNF_V2(3, 0, 0), CNF_V2(10, 0, 0),
     CNF_V2(10, 5, 0), CNF_V2(3, 5, 0),
+#endif
 };
 
 const V2Entry* find_v2(const Shape& s) {
