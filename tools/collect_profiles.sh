@@ -11,7 +11,7 @@ for d in gpurun_out/prof_${TAG}_*; do
   n=${d#gpurun_out/prof_${TAG}_}
   [ -f $d/run_kernel_stats.csv ] && cp $d/run_kernel_stats.csv profiles/${TAG}_${n}_kernel_stats.csv
 done
-for spec in "cfg2 loss k_sgpr 1048576" "cfg2 all k_sgpr 1048576" "cfg2 train k_vjp 1048576" "cfg4 forward k_wide 262144"; do
+for spec in "cfg2 loss k_sgpr 1048576" "cfg2 all k_valu 1048576" "cfg2 train k_vjp2 1048576" "cfg4 forward k_wide 262144" "cfg4 train k_wdw 262144"; do
   set -- $spec
   dir=gpurun_out/pmc_${TAG}_$1_$2_$1
   [ -d $dir ] || continue

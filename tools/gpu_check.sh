@@ -25,18 +25,19 @@ TAILN=2 run bench 600 python bench.py
 [ -n "$QUICK" ] && exit 0
 run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python bench.py --steps 100 --no-cpu-baseline --no-variants
 # one kernel-trace summary per profiled pass
-for spec in "cfg2 loss" "cfg2 forward" "cfg2 all" "cfg5 forward" "cfg4 forward" "cfg2 train"; do
+for spec in "cfg2 loss" "cfg2 forward" "cfg2 all" "cfg5 forward" "cfg4 forward" "cfg2 train" "cfg4 train"; do
   set -- $spec
   run rocprof_$1_$2 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_$1_$2 -o run --output-format csv -- python tools/prof_target.py --workload $1 --mode $2 --launches 30
 done
 # PMC passes: HBM traffic (separate FETCH / WRITE passes) and issue counters
 VALU="SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM GRBM_GUI_ACTIVE"
 MFMA="SQ_WAVES SQ_INSTS_VALU_MFMA_F32 SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE"
-for spec in "cfg2 loss k_sgpr" "cfg2 all k_sgpr" "cfg2 train k_vjp" "cfg4 forward k_wide"; do
+for spec in "cfg2 loss k_sgpr" "cfg2 all k_valu" "cfg2 train k_vjp2" "cfg4 forward k_wide" "cfg4 train k_wdw"; do
   set -- $spec
   rm -rf gpurun_out/pmc_${TAG}_$1_$2_$1
-  CTR="$VALU"; [ "$3" = "k_wide" ] && CTR="$MFMA"; [ "$3" = "k_vjp" ] && CTR="$MFMA"
-  run pmc_$1_$2 600 bash tools/gpu_pmc.sh ${TAG}_$1_$2 $1 "--mode $2 --launches 20" "FETCH_SIZE" "WRITE_SIZE" "$CTR"
+  CTR="$VALU"; case "$3" in k_wide|k_vjp2|k_wdw) CTR="$MFMA";; esac
+  NL=20; [ "$1 $2" = "cfg4 train" ] && NL=2
+  run pmc_$1_$2 600 bash tools/gpu_pmc.sh ${TAG}_$1_$2 $1 "--mode $2 --launches $NL" "FETCH_SIZE" "WRITE_SIZE" "$CTR"
   python tools/pmc_summary.py gpurun_out/pmc_${TAG}_$1_$2_$1 $3 > gpurun_out/${TAG}_pmc_$1_$2.txt 2>&1
 done
 exit 0
