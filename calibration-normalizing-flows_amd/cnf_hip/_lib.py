@@ -22,6 +22,8 @@ LOSS_CAL = 0
 LOSS_CE = 1
 OPT_NO_SGPR = 1   # cnf_desc.options (include/cnf.h)
 OPT_NO_WIDE = 2
+OPT_ALT_MASK = 4  # legacy code-old/realNVP.py semantics (flows/legacy.py)
+OPT_S_TANH = 8
 
 # Every symbol include/cnf.h declares (checked by tests/test_abi.py).
 EXPORTS = (

@@ -27,8 +27,11 @@ int derive_shape(const cnf_desc* d, Shape* s) {
   s->scale = d->scale;
   s->shift = d->shift;
   s->strict = d->strict_nan ? 1 : 0;
-  if (d->options & ~(CNF_OPT_NO_SGPR | CNF_OPT_NO_WIDE)) return CNF_ERR_DESC;
+  if (d->options & ~(CNF_OPT_NO_SGPR | CNF_OPT_NO_WIDE | CNF_OPT_ALT_MASK | CNF_OPT_S_TANH))
+    return CNF_ERR_DESC;
   s->options = d->options;
+  s->alt_mask = (d->options & CNF_OPT_ALT_MASK) != 0;
+  s->s_tanh = (d->options & CNF_OPT_S_TANH) != 0;
   s->nets = d->scale + d->shift;
   s->n_lin = d->n_hidden + 1;       // units = [dim] + hidden + [dim]  (flows/utils.py:14)
   s->units[0] = d->dim;
@@ -56,7 +59,10 @@ int derive_shape(const cnf_desc* d, Shape* s) {
       s->any_perm = true;
     }
   }
-  s->valu_id = s->D <= 16 ? valu_supported(*s) : -1;
+  if (s->alt_mask && s->any_perm) return CNF_ERR_DESC;
+  // legacy semantics: the MFMA-tile family only (ReLU / flip-only kernels elsewhere)
+  const bool legacy = s->alt_mask || s->s_tanh;
+  s->valu_id = s->D <= 16 && !legacy ? valu_supported(*s) : -1;
   if (s->valu_id >= 0) {
     s->family = Family::kValu;
     int64_t off = 0;

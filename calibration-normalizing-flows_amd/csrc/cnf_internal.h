@@ -25,6 +25,7 @@ struct Shape {
   int units[kMaxLin + 1] = {};       // [D, h..., D]
   int scale = 1, shift = 1, strict = 0;
   int options = 0;                   // cnf_desc.options (CNF_OPT_*)
+  bool alt_mask = false, s_tanh = false;  // legacy semantics (CNF_OPT_ALT_MASK / S_TANH)
   int nets = 2;                      // scale + shift
   int64_t net_floats = 0;            // natural layout (state_dict order)
   int64_t layer_floats = 0;

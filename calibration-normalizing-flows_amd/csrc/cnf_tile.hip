@@ -28,6 +28,7 @@ constexpr int kTileRows = 16;
 
 struct TileArgs {
   int D, DT, DC, NO, L, n_lin, scale, shift;
+  int s_act;                 // s-net hidden activation: 1 ReLU, 2 tanh (CNF_OPT_S_TANH)
   int nout[kMaxLin], OT[kMaxLin], KS[kMaxLin];
   int64_t lin_off[kMaxLin];  // float offset of linear i inside a tiled net
   int64_t net_floats, layer_floats;
@@ -47,15 +48,17 @@ __device__ __forceinline__ float relu(float a) {
   else return fmaxf(a, 0.f);
 }
 
+// act: 0 none (a net's last Linear), 1 ReLU, 2 tanh (legacy s-net)
 template <bool STRICT>
 __device__ __forceinline__ void epilogue(const floatx4& acc, int ot, const float* __restrict__ bias,
-                                         float* OUT, int nout, bool do_relu, float p0, int lane) {
+                                         float* OUT, int nout, int act, float p0, int lane) {
   const int c = lane & 15, g = lane >> 4;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int o = ot * 16 + 4 * g + r;
     float v = acc[r] + bias[o] + p0;
-    if (do_relu) v = relu<STRICT>(v);
+    if (act == 1) v = relu<STRICT>(v);
+    else if (act == 2) v = tanhf(v);
     OUT[o * kTileRows + c] = o < nout ? v : 0.f;
   }
 }
@@ -63,7 +66,7 @@ __device__ __forceinline__ void epilogue(const floatx4& acc, int ot, const float
 // OUT[o][j] = act(bias[o] + sum_k W[o][k] * IN[k][j]) for o < OT*16, j < 16.
 template <bool STRICT>
 __device__ __forceinline__ void gemm(const float* __restrict__ lin, const float* IN, float* OUT,
-                                     int OT, int KS, int nout, bool do_relu, float p0, int lane) {
+                                     int OT, int KS, int nout, int act, float p0, int lane) {
   const float* __restrict__ bias = lin;
   const float* __restrict__ tiles = lin + OT * 16;
   const int boff = (lane >> 4) * kTileRows + (lane & 15);
@@ -85,8 +88,8 @@ __device__ __forceinline__ void gemm(const float* __restrict__ lin, const float*
         acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(w0[ks * 64], b, acc0, 0, 0, 0);
       }
     }
-    epilogue<STRICT>(acc0, ot, bias, OUT, nout, do_relu, p0, lane);
-    if (two) epilogue<STRICT>(acc1, ot + 1, bias, OUT, nout, do_relu, p0, lane);
+    epilogue<STRICT>(acc0, ot, bias, OUT, nout, act, p0, lane);
+    if (two) epilogue<STRICT>(acc1, ot + 1, bias, OUT, nout, act, p0, lane);
   }
 }
 
@@ -94,12 +97,12 @@ __device__ __forceinline__ void gemm(const float* __restrict__ lin, const float*
 template <bool STRICT>
 __device__ __forceinline__ void mlp(const TileArgs& a, const float* __restrict__ net,
                                     const float* Xc, float* A0, float* A1, float* OUT, float p0,
-                                    int lane) {
+                                    int lane, int act) {
   const float* in = Xc;
   for (int i = 0; i < a.n_lin; ++i) {
     const bool last = i == a.n_lin - 1;
     float* o = last ? OUT : ((i & 1) ? A1 : A0);
-    gemm<STRICT>(net + a.lin_off[i], in, o, a.OT[i], a.KS[i], a.nout[i], !last,
+    gemm<STRICT>(net + a.lin_off[i], in, o, a.OT[i], a.KS[i], a.nout[i], last ? 0 : act,
                  i == 0 ? p0 : 0.f, lane);
     wave_sync();
     in = o;
@@ -153,10 +156,10 @@ __global__ __launch_bounds__(256) void k_tile(TileArgs a, const float* __restric
     }
     const float* __restrict__ wl = W + (int64_t)l * a.layer_floats;
     if (a.scale) {
-      mlp<STRICT>(a, wl, X + DT * kTileRows, A0, A1, S, p0, lane);
+      mlp<STRICT>(a, wl, X + DT * kTileRows, A0, A1, S, p0, lane, a.s_act);
       wl += a.net_floats;
     }
-    if (a.shift) mlp<STRICT>(a, wl, X + DT * kTileRows, A0, A1, T, p0, lane);
+    if (a.shift) mlp<STRICT>(a, wl, X + DT * kTileRows, A0, A1, T, p0, lane, 1);
     const int nupd = STRICT ? D : DT;
     for (int i = lane; i < nupd * kTileRows; i += 64) {
       const int j = i >> 4;
@@ -205,6 +208,7 @@ TileArgs make_args(const Shape& s) {
   TileArgs a{};
   a.D = s.D; a.DT = s.DT; a.DC = s.DC; a.NO = s.NO; a.L = s.L; a.n_lin = s.n_lin;
   a.scale = s.scale; a.shift = s.shift;
+  a.s_act = s.s_tanh ? 2 : 1;
   for (int i = 0; i < s.n_lin; ++i) {
     a.nout[i] = s.lin_nout[i];
     a.OT[i] = s.lin_OT[i];
@@ -230,6 +234,7 @@ struct PrepSeg {
   int64_t dst;  // float offset in the weights region
   int mode;     // 0: natural copy, 1: MFMA tiles, 2: compact (VALU), 3: packed (SGPR)
   int nout_full, nin_full, in_off, nin, nout, OT, KS;
+  int rev_in, rev_out;  // legacy alternate mask, odd layer: input columns / output rows reversed
   float wmul, bmul;  // mode 3: weights / bias scale (relu clamp 2^-64, log2 e; cnf_sgpr.hip)
 };
 
@@ -251,10 +256,18 @@ __global__ void k_prepare(PrepArgs a, float* __restrict__ wreg, int32_t* __restr
   }
   const PrepSeg& g = a.seg[blockIdx.x];
   float* dst = wreg + g.dst;
+  auto orow = [&](int o) { return g.rev_out ? g.nout_full - 1 - o : o; };
+  auto icol = [&](int c) { return g.rev_in ? g.nin_full - 1 - c : c; };
   if (g.mode == 0) {
     const int64_t nW = (int64_t)g.nout_full * g.nin_full;
-    for (int64_t i = threadIdx.x; i < nW + g.nout_full; i += blockDim.x)
-      dst[i] = i < nW ? g.W[i] : g.b[i - nW];
+    for (int64_t i = threadIdx.x; i < nW + g.nout_full; i += blockDim.x) {
+      if (i < nW) {
+        const int o = (int)(i / g.nin_full), c = (int)(i - (int64_t)o * g.nin_full);
+        dst[i] = g.W[(int64_t)orow(o) * g.nin_full + icol(c)];
+      } else {
+        dst[i] = g.b[orow((int)(i - nW))];
+      }
+    }
     return;
   }
   if (g.mode == 3) {  // rows [w_o0, b_o, w_o1 .. w_o(nin-1)] at even stride, zero padded
@@ -289,7 +302,7 @@ __global__ void k_prepare(PrepArgs a, float* __restrict__ wreg, int32_t* __restr
     }
     return;
   }
-  for (int o = threadIdx.x; o < g.OT * 16; o += blockDim.x) dst[o] = o < g.nout ? g.b[o] : 0.f;
+  for (int o = threadIdx.x; o < g.OT * 16; o += blockDim.x) dst[o] = o < g.nout ? g.b[orow(o)] : 0.f;
   const int64_t ntile = (int64_t)g.OT * g.KS * 64;
   float* tiles = dst + g.OT * 16;
   for (int64_t e = threadIdx.x; e < ntile; e += blockDim.x) {
@@ -297,7 +310,8 @@ __global__ void k_prepare(PrepArgs a, float* __restrict__ wreg, int32_t* __restr
     const int rem = (int)(e - ot * g.KS * 64);
     const int ks = rem >> 6, ln = rem & 63;
     const int o = (int)ot * 16 + (ln & 15), k = ks * 4 + (ln >> 4);
-    tiles[e] = (o < g.nout && k < g.nin) ? g.W[(int64_t)o * g.nin_full + g.in_off + k] : 0.f;
+    tiles[e] = (o < g.nout && k < g.nin)
+                   ? g.W[(int64_t)orow(o) * g.nin_full + icol(g.in_off + k)] : 0.f;
   }
 }
 
@@ -385,6 +399,11 @@ int prepare_run(const Shape& s, const float* const* params, void* prepared, hipS
         if (!g.W || !g.b) return CNF_ERR_NULL;
         g.nout_full = s.units[i + 1];
         g.nin_full = s.units[i];
+        g.rev_in = g.rev_out = 0;
+        if (tiled && s.alt_mask && (l & 1)) {
+          g.rev_in = i == 0;
+          g.rev_out = i == s.n_lin - 1;
+        }
         if (tiled) {
           g.mode = 1;
           g.in_off = s.lin_inoff[i];
@@ -413,10 +432,16 @@ int prepare_run(const Shape& s, const float* const* params, void* prepared, hipS
     if (perm) {
       for (int j = 0; j < s.D; ++j) rev[perm[j]] = j;
     }
+    // legacy alternate mask (no data flip): the flip-based stack with odd
+    // layers' weights reversed computes flip^(l+1) of the legacy layer l
+    // output, so an odd-L stack ends with one extra flip: its last table is
+    // the identity
+    const bool unflip = s.alt_mask && (s.L & 1) && l == s.L - 1;
+    if (unflip) a.flag = kFlagPerm;
     for (int j = 0; j < s.D; ++j) {
       // forward: out[j] = z[perm[D-1-j]]; inverse: x_in[j] = z[D-1-rev_perm[j]]
-      a.fq[j] = perm ? (int32_t)perm[s.D - 1 - j] : s.D - 1 - j;
-      a.iq[j] = perm ? s.D - 1 - rev[j] : s.D - 1 - j;
+      a.fq[j] = unflip ? j : (perm ? (int32_t)perm[s.D - 1 - j] : s.D - 1 - j);
+      a.iq[j] = unflip ? j : (perm ? s.D - 1 - rev[j] : s.D - 1 - j);
     }
     hipLaunchKernelGGL(k_prepare, dim3(a.nseg + 1), dim3(256), 0, st, a, wreg, idx);
     if (tiled) {

@@ -434,7 +434,8 @@ int64_t wide_layer_floats(const Shape& s) {
 // Final-output forward / inverse of shift-on, non-strict stacks in the table;
 // every-layer outputs and strict_nan stay on k_tile.
 bool wide_ok(const Shape& s) {
-  return wfind(s) && s.shift && !s.strict && !(s.options & CNF_OPT_NO_WIDE);
+  return wfind(s) && s.shift && !s.strict && !s.alt_mask && !s.s_tanh &&
+         !(s.options & CNF_OPT_NO_WIDE);
 }
 
 int wide_prepare(const Shape& s, const float* const* params, void* prepared, hipStream_t st) {

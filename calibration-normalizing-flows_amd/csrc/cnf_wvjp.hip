@@ -73,6 +73,7 @@ struct GemmJob {
   float* C;
   int64_t lda, lda2, ldm, ldc;
   int ldb, ldb2, N, K, ldw, ones;
+  int act;  // hidden activation of this net: 1 ReLU, 2 tanh (legacy s-net, CNF_OPT_S_TANH)
 };
 struct GemmArgs {
   GemmJob job[2];  // one per conditioner net (grid.z)
@@ -192,8 +193,15 @@ __global__ __launch_bounds__(256, PAIR ? 3 : 4) void k_wgemm(GemmArgs ga) {
         if (m >= M) continue;
         float v = acc[c][q];
         if constexpr (EPI == kEpiBias || EPI == kEpiBiasRelu) v += b;
-        if constexpr (EPI == kEpiBiasRelu) v = v < 0.f ? 0.f : v;  // keeps NaN (torch relu)
-        if constexpr (EPI == kEpiMask) v = real && j.mask[m * j.ldm + n] > 0.f ? v : 0.f;
+        if constexpr (EPI == kEpiBiasRelu) {  // the hidden activation
+          if (j.act == 2) v = tanhf(v);
+          else v = v < 0.f ? 0.f : v;  // keeps NaN (torch relu)
+        }
+        if constexpr (EPI == kEpiMask) {  // its derivative from the stored output h
+          const float h = real ? j.mask[m * j.ldm + n] : 0.f;
+          v = j.act == 2 ? v * (1.f - h * h) : (h > 0.f ? v : 0.f);
+          if (!real) v = 0.f;
+        }
         if constexpr (EPI == kEpiAdd) v += j.C[m * j.ldc + n];
         j.C[m * j.ldc + n] = real ? v : pad;
       }
@@ -233,6 +241,9 @@ struct DwJob {
   int64_t ldg, ldh;
   int64_t woff, boff;  // float offsets of W[0][in_off] and b[0] in the layer record
   int wld, N, K, tiles_k;
+  int cstep;           // +1, or -1 when the kernel's input columns run reversed (legacy)
+  int rrev;            // output rows reversed (legacy): row n is parameter row N_full-1-n
+  int nfull;
 };
 struct DwArgs {
   DwJob job[2 * kMaxLin];
@@ -314,8 +325,9 @@ __global__ __launch_bounds__(64) void k_wdw(DwArgs da) {
     for (int q = 0; q < 16; ++q) {
       const int nn = n0 + (q & 3) + 8 * (q >> 2) + 4 * h;
       if (nn >= j.N) continue;
-      if (k < j.K) out[j.woff + (int64_t)nn * j.wld + k] = acc[c][q];
-      else out[j.boff + nn] = acc[c][q];
+      const int pr = j.rrev ? j.nfull - 1 - nn : nn;  // parameter row
+      if (k < j.K) out[j.woff + (int64_t)pr * j.wld + (int64_t)j.cstep * k] = acc[c][q];
+      else out[j.boff + pr] = acc[c][q];
     }
   }
 }
@@ -683,6 +695,7 @@ int wvjp_run(const Shape& s, const void* prepared, const float* x, const int64_t
         j.ldc = last ? geom.DTp : hp(s, k);
         j.ldw = last ? j.N : hp(s, k);
         j.ones = !last;
+        j.act = (s.s_tanh && s.scale && n == 0) ? 2 : 1;
       }
       gemm(ga, B, ga.job[0].ldw, lin_in(s, k), s.nets, true, last ? kEpiBias : kEpiBiasRelu,
            false, st);
@@ -737,6 +750,7 @@ int wvjp_run(const Shape& s, const void* prepared, const float* x, const int64_t
         j.ldw = gp(s, k - 1);
         j.mask = W + p.H[n][k - 1];
         j.ldm = hp(s, k - 1);
+        j.act = (s.s_tanh && s.scale && n == 0) ? 2 : 1;
       }
       gemm(ga, B, gp(s, k - 1), lin_out(s, k), s.nets, false, kEpiMask, false, st);
     }
@@ -761,7 +775,13 @@ int wvjp_run(const Shape& s, const void* prepared, const float* x, const int64_t
       j.ldw = DC;
       gemm(ga, B, DC, j.K, 1, false, kEpiAdd, s.nets == 2, st);
     }
-    // weight / bias gradients of every Linear of both nets: one launch
+    // weight / bias gradients of every Linear of both nets: one launch.  The
+    // partial records are reused across layers: positions a layer never writes
+    // (masked columns / rows) keep the zeros of the memset, except that under
+    // the legacy alternate mask odd and even layers mask different positions
+    if (s.alt_mask && l < L - 1 &&
+        hipMemsetAsync(part, 0, (size_t)p.nkb * PS * 4, st) != hipSuccess)
+      return check_launch();
     DwArgs da{};
     da.partials = part;
     da.M = B;
@@ -777,7 +797,15 @@ int wvjp_run(const Shape& s, const void* prepared, const float* x, const int64_t
         j.ldh = k == 0 ? Dp : hp(s, k - 1);
         j.N = lin_out(s, k);
         j.K = lin_in(s, k);
-        j.woff = n * s.net_floats + lin_off(s, k) + (k == 0 ? DT : 0);
+        // legacy alternate mask: an odd layer's kernel weights are its
+        // parameters with the first Linear's columns and the last Linear's
+        // rows reversed (cnf_tile.hip prepare); map the gradients back
+        const bool rev = s.alt_mask && (l & 1);
+        const bool rin = rev && k == 0, rout = rev && k == NL - 1;
+        j.cstep = rin ? -1 : 1;
+        j.rrev = rout;
+        j.nfull = s.units[k + 1];
+        j.woff = n * s.net_floats + lin_off(s, k) + (k == 0 ? (rin ? D - 1 - DT : DT) : 0);
         j.wld = s.units[k];
         j.boff = n * s.net_floats + lin_off(s, k) + (int64_t)s.units[k + 1] * s.units[k];
         j.tiles_k = (j.K + 1 + kDwCols - 1) / kDwCols;

@@ -70,6 +70,18 @@ typedef struct cnf_desc {
  * results agree to fp32 rounding either way). */
 #define CNF_OPT_NO_SGPR 1   /* narrow flows: k_valu instead of k_sgpr          */
 #define CNF_OPT_NO_WIDE 2   /* wide flows: k_tile instead of k_wide            */
+/* Legacy semantics of the reference's TensorFlow flows (code-old/realNVP.py:
+ * 19-92; parity unpinned -- TensorFlow is absent):
+ *   ALT_MASK  the coupling mask alternates per layer (layer l transforms the
+ *             first D//2 features when l is even, the last D//2 when l is
+ *             odd) and the data are never flipped (code-old/realNVP.py:66-76);
+ *             parameters keep the layer's own column / row order;
+ *   S_TANH    the s-net's hidden activations are tanh (code-old/realNVP.py:
+ *             58-64); the t-net keeps ReLU.
+ * Served by the MFMA-tile family (forward / inverse) and its reverse mode;
+ * not combinable with random_flip permutations. */
+#define CNF_OPT_ALT_MASK 4
+#define CNF_OPT_S_TANH 8
 
 /* One float per parameter, in the reference's state_dict order. */
 int cnf_param_count(const cnf_desc* desc, int64_t* n_floats);
