@@ -167,7 +167,13 @@ class TorchFlowCalibrator(Calibrator):
         """Same schedule on the fused kernels: one cnf_loss_vjp launch per
         training batch, one cnf_forward_loss launch per evaluation batch."""
         from cnf_hip import vjp as V
-        params = stack.param_tensors()
+        from cnf_hip.adam import StackAdam
+        # the optimizer step on the device in one launch (the torch Adam's
+        # hyper-parameters), straight from the fused step's flat gradient
+        adam = getattr(self, "_stack_adam", None)
+        if adam is None or adam.stack is not stack:
+            adam = StackAdam.like(stack, self.optimizer)
+            self._stack_adam = adam
         N = logits.shape[0]
         history = {'loss': [], 'ce': [], 'log_det': []}
         gen = torch.Generator(device=logits.device)
@@ -179,9 +185,7 @@ class TorchFlowCalibrator(Calibrator):
                 idx = order[s:s + batch_size]
                 xb, yb = logits.index_select(0, idx), target.index_select(0, idx)
                 _, grads, _ = V.loss_and_grads(stack, xb, yb, grad_scale=1.0 / xb.shape[0])
-                for p, g in zip(params, V._split(stack, grads)):
-                    p.grad = g
-                self.optimizer.step()
+                adam.step(grads)
             self.flow.eval()
             order = torch.randperm(N, device=logits.device, generator=gen)
             num = 0
@@ -194,8 +198,6 @@ class TorchFlowCalibrator(Calibrator):
             history['loss'].append(terms[0] / num)
             history['ce'].append(terms[1] / num)
             history['log_det'].append(terms[2] / num)
-        for p in params:
-            p.grad = None
         return history
 
     # -------------------------------------------------------------- predict

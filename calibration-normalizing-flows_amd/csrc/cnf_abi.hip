@@ -86,6 +86,9 @@ int derive_shape(const cnf_desc* d, Shape* s) {
     s->sp_net_floats = off;
     s->sp_region = s->valu_net_floats * s->nets * s->L;
     s->vp_region = s->sp_region + s->sp_net_floats * s->nets * s->L;
+    // natural copy for the layer-at-a-time reverse mode (shapes k_vjp2 / k_vjp
+    // do not cover: L > 8, wide hidden layers)
+    s->plain_region = s->sp_region + (s->sp_ok ? 2 * s->sp_net_floats * s->nets * s->L : 0);
   } else {
     s->family = Family::kTile;
     int st = tile_configure(s);
@@ -143,7 +146,8 @@ int cnf_prepared_bytes(const cnf_desc* desc, size_t* bytes) {
   const int64_t wf = s.family == Family::kTile
                        ? s.tile_layer_floats * s.L + s.wide_floats + s.layer_floats * s.L
                        : s.valu_net_floats * s.nets * s.L +
-                             (s.sp_ok ? 2 * s.sp_net_floats * s.nets * s.L : 0);
+                             (s.sp_ok ? 2 * s.sp_net_floats * s.nets * s.L : 0) +
+                             s.layer_floats * s.L;
   // +256: scalar-cache prefetch reads whole 64-B lines past the last weight
   *bytes = (size_t)(idx_bytes(s) + wf * 4 + 256);
   return CNF_OK;

@@ -444,7 +444,7 @@ int prepare_run(const Shape& s, const float* const* params, void* prepared, hipS
       a.iq[j] = unflip ? j : (perm ? s.D - 1 - rev[j] : s.D - 1 - j);
     }
     hipLaunchKernelGGL(k_prepare, dim3(a.nseg + 1), dim3(256), 0, st, a, wreg, idx);
-    if (tiled) {
+    {
       // natural copy of the layer (state_dict order) for the reverse mode
       PrepArgs c = a;
       int64_t d = s.plain_region + (int64_t)l * s.layer_floats;

@@ -1260,6 +1260,10 @@ size_t v2_stash_offset(const Shape& s, int64_t nblk) {
 
 int vjp_workspace(const Shape& s, int64_t B, size_t* bytes) {
   if (s.family == Family::kTile) return wvjp_workspace(s, B, bytes);
+  if (!find_v2(s)) {  // narrow shapes outside both row-resident kernels
+    const VEntry* e = find_entry(s);
+    if (!e || lds_bytes(s, *e) > 64 * 1024) return wvjp_workspace(s, B, bytes);
+  }
   if (const V2Entry* e2 = find_v2(s)) {
     // the larger of the two variants (loss / generic) -- same grid rule
     const int64_t g = std::max(grid_v2(s, pick_v2(e2, s, true), B),
@@ -1277,7 +1281,12 @@ int vjp_run(const Shape& s, const void* prepared, const float* x, const int64_t*
             const float* gz, const float* gz_all, const float* gld, int kind, float det,
             float grad_scale, float* loss_terms, float* grads, float* dx, int64_t B, void* ws,
             size_t ws_bytes, hipStream_t st) {
-  if (s.family == Family::kTile)
+  bool layerwise = s.family == Family::kTile;
+  if (!layerwise && !find_v2(s)) {
+    const VEntry* e = find_entry(s);
+    layerwise = !e || lds_bytes(s, *e) > 64 * 1024;
+  }
+  if (layerwise)
     return wvjp_run(s, prepared, x, y, gz, gz_all, gld, kind, det, grad_scale, loss_terms, grads,
                     dx, B, ws, ws_bytes, st);
   if (const V2Entry* e2 = find_v2(s)) {

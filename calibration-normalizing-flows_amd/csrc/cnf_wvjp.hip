@@ -537,9 +537,16 @@ Geo geo(const Shape& s) {
 struct Plan {
   int64_t stash, ld, gld, g0, g1, seed, part;
   int64_t H[2][kMaxLin], O[2], G[2][kMaxLin];
+  int64_t act_stride;  // floats between layers' H / O (keep_acts), else 0
+  bool keep_acts;      // every layer's conditioner activations kept from the forward sweep
   int64_t total;
   int64_t nkb, rows_kb, nseed;
 };
+
+// Keeping every layer's conditioner activations (instead of recomputing them
+// in the backward sweep) costs no extra HBM traffic -- the forward sweep
+// writes them anyway -- only workspace; kept up to this many bytes.
+constexpr double kKeepActsBytes = 8.0 * (1 << 30);
 
 Plan make_plan(const Shape& s, int64_t B) {
   Plan p{};
@@ -556,11 +563,25 @@ Plan make_plan(const Shape& s, int64_t B) {
   p.gld = take(Bn);
   p.g0 = take(Bn * s.D);
   p.g1 = take(Bn * s.D);
+  int64_t acts = 0;  // floats of one layer's H / O, all nets
   for (int n = 0; n < s.nets; ++n) {
-    for (int k = 0; k + 1 < s.n_lin; ++k) p.H[n][k] = take(Bn * hp(s, k));
-    p.O[n] = take(Bn * g.DTp);
-    for (int k = 0; k < s.n_lin; ++k) p.G[n][k] = take(Bn * gp(s, k));
+    for (int k = 0; k + 1 < s.n_lin; ++k) acts += al64(Bn * hp(s, k));
+    acts += al64(Bn * g.DTp);
   }
+  p.keep_acts = s.L > 1 && (double)acts * s.L * 4 <= kKeepActsBytes;
+  p.act_stride = p.keep_acts ? acts : 0;
+  const int64_t act0 = take(acts * (p.keep_acts ? s.L : 1));
+  int64_t a = act0;
+  for (int n = 0; n < s.nets; ++n) {
+    for (int k = 0; k + 1 < s.n_lin; ++k) {
+      p.H[n][k] = a;
+      a += al64(Bn * hp(s, k));
+    }
+    p.O[n] = a;
+    a += al64(Bn * g.DTp);
+  }
+  for (int n = 0; n < s.nets; ++n)
+    for (int k = 0; k < s.n_lin; ++k) p.G[n][k] = take(Bn * gp(s, k));
   p.nseed = std::min<int64_t>(1024, (Bn + 15) / 16);
   p.seed = take(p.nseed * 4);
   int64_t rows = (Bn + 255) / 256;
@@ -630,7 +651,7 @@ void gemm(const GemmArgs& ga, int64_t B, int cols, int K, int nz, bool bt, int e
 // launch) must fit one CU's LDS: widths up to ~290 (CNF_MAX_WIDTH 512 shapes
 // beyond that keep the torch fallback).
 bool wvjp_ok(const Shape& s) {
-  if (s.family != Family::kTile || s.strict) return false;
+  if (s.strict) return false;
   constexpr size_t kLds = 160 * 1024;
   for (int k = 0; k < s.n_lin; ++k) {
     const int cols = k == s.n_lin - 1 ? s.DT : hp(s, k);
@@ -677,6 +698,9 @@ int wvjp_run(const Shape& s, const void* prepared, const float* x, const int64_t
   const unsigned wave_blocks = (unsigned)std::min<int64_t>((B + 3) / 4, 16384);
 
   // conditioner forward of layer l from its stashed input: H[n][k], O[n]
+  // layer l's conditioner activations (one shared set unless keep_acts)
+  auto Hb = [&](int l, int n, int k) { return W + p.H[n][k] + (int64_t)l * p.act_stride; };
+  auto Ob = [&](int l, int n) { return W + p.O[n] + (int64_t)l * p.act_stride; };
   auto nets_forward = [&](int l) {
     for (int k = 0; k < NL; ++k) {
       GemmArgs ga{};
@@ -684,14 +708,14 @@ int wvjp_run(const Shape& s, const void* prepared, const float* x, const int64_t
       const bool last = k == NL - 1;
       for (int n = 0; n < s.nets; ++n) {
         GemmJob& j = ga.job[n];
-        j.A = k == 0 ? Xs(l) : W + p.H[n][k - 1];
+        j.A = k == 0 ? Xs(l) : Hb(l, n, k - 1);
         j.lda = k == 0 ? Dp : hp(s, k - 1);
         j.K = lin_in(s, k);
         j.Bw = wptr(l, n, k) + (k == 0 ? DT : 0);
         j.ldb = s.units[k];
         j.N = lin_out(s, k);
         j.bias = bptr(l, n, k);
-        j.C = last ? W + p.O[n] : W + p.H[n][k];
+        j.C = last ? Ob(l, n) : Hb(l, n, k);
         j.ldc = last ? geom.DTp : hp(s, k);
         j.ldw = last ? j.N : hp(s, k);
         j.ones = !last;
@@ -701,15 +725,15 @@ int wvjp_run(const Shape& s, const void* prepared, const float* x, const int64_t
            false, st);
     }
   };
-  const float* Os = s.scale ? W + p.O[0] : nullptr;
-  const float* Ot = s.shift ? W + p.O[s.scale] : nullptr;
+  auto Os = [&](int l) -> const float* { return s.scale ? Ob(l, 0) : nullptr; };
+  auto Ot = [&](int l) -> const float* { return s.shift ? Ob(l, s.scale) : nullptr; };
 
   // ---- forward sweep ----
   hipLaunchKernelGGL(k_wstash, dim3(wave_blocks), dim3(256), 0, st, x, Xs(0), B, geom);
   for (int l = 0; l < L; ++l) {
     if (s.nets) nets_forward(l);
     hipLaunchKernelGGL(k_wfwd_update, dim3(wave_blocks), dim3(256), 0, st, Xs(l), Xs(l + 1), ld,
-                       Os, Ot, fq + l * D, B, geom, l == 0);
+                       Os(l), Ot(l), fq + l * D, B, geom, l == 0);
   }
   // ---- seed ----
   float* g[2] = {W + p.g0, W + p.g1};
@@ -723,11 +747,11 @@ int wvjp_run(const Shape& s, const void* prepared, const float* x, const int64_t
 
   // ---- backward sweep ----
   for (int l = L - 1; l >= 0; --l) {
-    if (s.nets) nets_forward(l);
+    if (s.nets && !p.keep_acts) nets_forward(l);  // recompute, or the kept activations
     float* gin = (l == 0 && dx) ? dx : g[cur ^ 1];
     float* Gs = s.scale ? W + p.G[0][NL - 1] : nullptr;
     float* Gt = s.shift ? W + p.G[s.scale][NL - 1] : nullptr;
-    hipLaunchKernelGGL(k_wbwd_update, dim3(wave_blocks), dim3(256), 0, st, g[cur], gin, Xs(l), Os,
+    hipLaunchKernelGGL(k_wbwd_update, dim3(wave_blocks), dim3(256), 0, st, g[cur], gin, Xs(l), Os(l),
                        gld, Gs, Gt, gz_all && l > 0 ? gz_all + (int64_t)(l - 1) * B * D : nullptr,
                        fq + l * D, B, geom);
     if (s.nets == 0) {
@@ -748,7 +772,7 @@ int wvjp_run(const Shape& s, const void* prepared, const float* x, const int64_t
         j.C = W + p.G[n][k - 1];
         j.ldc = gp(s, k - 1);
         j.ldw = gp(s, k - 1);
-        j.mask = W + p.H[n][k - 1];
+        j.mask = Hb(l, n, k - 1);
         j.ldm = hp(s, k - 1);
         j.act = (s.s_tanh && s.scale && n == 0) ? 2 : 1;
       }
@@ -793,7 +817,7 @@ int wvjp_run(const Shape& s, const void* prepared, const float* x, const int64_t
         DwJob& j = da.job[jobs++];
         j.G = W + p.G[n][k];
         j.ldg = gp(s, k);
-        j.H = k == 0 ? Xs(l) : W + p.H[n][k - 1];
+        j.H = k == 0 ? Xs(l) : Hb(l, n, k - 1);
         j.ldh = k == 0 ? Dp : hp(s, k - 1);
         j.N = lin_out(s, k);
         j.K = lin_in(s, k);

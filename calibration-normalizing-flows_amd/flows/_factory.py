@@ -33,13 +33,3 @@ class CouplingFlow(Flow):
     def forward_all(self, x):
         """The reference Flow.forward: (zs list, cum_log_det)."""
         return Flow.forward(self, x)
-
-
-class RealNvpFlow(CouplingFlow):
-    """RealNVP affine coupling stack (s-net and t-net)."""
-    scale = True
-
-
-class NiceFlow(CouplingFlow):
-    """NICE additive coupling stack (t-net only, log-det = 0)."""
-    scale = False

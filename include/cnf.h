@@ -178,6 +178,18 @@ int cnf_loss_vjp(const cnf_desc* desc, const void* prepared, const float* x,
  * shapes whose Linears exceed 32 floats, misaligned views), "mfma-wide"
  * (register-resident MFMA, the wide shapes of its table), "mfma-tile" (other
  * wide shapes, every-layer outputs of wide stacks). */
+/* One Adam step over every parameter (torch.optim.Adam's update, amsgrad off;
+ * the optimizer of TorchFlowCalibrator.fit, calibrators.py:239-295) in one
+ * launch, fed by the flat gradient of cnf_loss_vjp / cnf_vjp:
+ *   params      HOST array of cnf_param_tensor_count DEVICE pointers, updated
+ *               in place (the tensors cnf_prepare reads)
+ *   grads       [cnf_param_count]  flat, state_dict order
+ *   exp_avg, exp_avg_sq  [cnf_param_count] moments, zero before step 1
+ *   step        1-based step count (bias corrections) */
+int cnf_adam_step(const cnf_desc* desc, float* const* params, const float* grads,
+                  float* exp_avg, float* exp_avg_sq, int64_t step, float lr, float beta1,
+                  float beta2, float eps, float weight_decay, void* stream);
+
 const char* cnf_kernel_name(const cnf_desc* desc);
 
 const char* cnf_strerror(int status);

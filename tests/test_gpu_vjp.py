@@ -86,6 +86,7 @@ def _flow(D, L, hidden, sigma, seed, scale=True, shift=True, flip=False):
     (10, 3, [5, 5], True, False, False),   # shift=False
     (10, 3, [], True, True, False),
     (10, 3, [7], True, True, False),
+    (10, 12, [5, 5], True, True, True),   # L > 8: the layerwise reverse mode (cnf_wvjp.hip)
     # the MFMA family's layer-at-a-time reverse mode (cnf_wvjp.hip)
     (10, 3, [4, 6, 3], True, True, False),
     (20, 3, [24, 16], True, True, True),

@@ -64,3 +64,20 @@ def test_alternate_mask_equals_flipped_stack_with_reversed_weights(D, L):
     zs, ld2 = ref(x)
     z = zs[-1].flip(1) if L & 1 else zs[-1]
     assert torch.allclose(y, z, atol=1e-12) and torch.allclose(ld, ld2, atol=1e-12)
+
+
+def test_factory_options_select_the_legacy_flow():
+    """flows.realNVP_torch.RealNvpFlow: mask_mode / s_activation."""
+    from flows.legacy import LegacyRealNvpFlow as LF
+    from flows.realNVP_torch import RealNvpFlow
+    f = RealNvpFlow(6, layers=3, hidden_size=[4], mask_mode="alternate_mask",
+                    s_activation="tanh", dev="cpu", epochs=3)
+    assert isinstance(f, LF) and len(f.layers) == 3 and f.layers[0].s_activation == "tanh"
+    y, ld = f(torch.randn(5, 6))
+    assert y.shape == (5, 6) and ld.shape == (5,)
+    g = RealNvpFlow(6, layers=2)  # the maintained flow, (z_final, ld)
+    assert isinstance(g, RealNvpFlow) and not isinstance(g, LF)
+    z, ld = g(torch.randn(5, 6))
+    assert z.shape == (5, 6)
+    with pytest.raises(ValueError):
+        RealNvpFlow(6, mask_mode="bogus")
