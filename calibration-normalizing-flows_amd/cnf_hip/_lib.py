@@ -30,6 +30,7 @@ EXPORTS = (
     "cnf_param_count", "cnf_param_tensor_count", "cnf_prepared_bytes", "cnf_prepare",
     "cnf_forward", "cnf_inverse", "cnf_forward_loss_workspace_bytes", "cnf_forward_loss",
     "cnf_predict", "cnf_vjp_workspace_bytes", "cnf_vjp", "cnf_loss_vjp", "cnf_adam_step",
+    "cnf_vjp_inverse_workspace_bytes", "cnf_vjp_inverse",
     "cnf_kernel_name", "cnf_strerror", "cnf_last_hip_error", "cnf_abi_version",
 )
 
@@ -86,6 +87,9 @@ def _bind(lib):
         "cnf_vjp": (ctypes.c_int, [D, P, P, P, P, P, P, P, I64, P, ctypes.c_size_t, P]),
         "cnf_loss_vjp": (ctypes.c_int, [D, P, P, P, I32, F, F, P, P, P, I64, P, ctypes.c_size_t,
                                         P]),
+        "cnf_vjp_inverse_workspace_bytes": (ctypes.c_int,
+                                            [D, I64, ctypes.POINTER(ctypes.c_size_t)]),
+        "cnf_vjp_inverse": (ctypes.c_int, [D, P, P, P, P, P, P, P, I64, P, ctypes.c_size_t, P]),
         "cnf_adam_step": (ctypes.c_int, [D, ctypes.POINTER(P), P, P, P, I64, F, F, F, F, F, P]),
         "cnf_kernel_name": (ctypes.c_char_p, [D]),
         "cnf_strerror": (ctypes.c_char_p, [ctypes.c_int]),

@@ -284,6 +284,45 @@ class CouplingStack:
         return _StackFn.apply(self, want_all, x, *ps)
 
 
+    def inverse_autograd(self, z, want_all):
+        """Inverse with gradients w.r.t. z and every parameter
+        (cnf_vjp_inverse, the layer-at-a-time reverse mode)."""
+        return _InvStackFn.apply(self, want_all, z, *self.param_tensors())
+
+
+class _InvStackFn(torch.autograd.Function):
+    """Flow.backward (the inverse transform) under autograd: cnf_inverse
+    forward, cnf_vjp_inverse backward."""
+
+    @staticmethod
+    def forward(ctx, stack, want_all, z, *params):
+        blob = stack.prepared(z.device)
+        fin, ld, allt = stack.run(z, inverse=True, want_all=want_all, blob=blob)
+        ctx.stack = stack
+        ctx.want_all = want_all
+        ctx.blob = blob
+        ctx.key = stack.state_key()
+        ctx.save_for_backward(z)
+        return (allt if want_all else fin), ld
+
+    @staticmethod
+    def backward(ctx, g_out, g_ld):
+        from .vjp import stack_vjp_inverse
+        (z,) = ctx.saved_tensors
+        stack = ctx.stack
+        if stack.state_key() != ctx.key:
+            raise RuntimeError(
+                "one of the variables needed for gradient computation has been modified by an "
+                "inplace operation: a coupling-layer weight or permutation changed between the "
+                "native inverse and its backward")
+        dz, grads = stack_vjp_inverse(stack, z, g_out, g_ld, all_grads=ctx.want_all,
+                                      need_dz=ctx.needs_input_grad[2], blob=ctx.blob)
+        out = [None, None, dz]
+        for p, g in zip(stack.param_tensors(), grads):
+            out.append(g.view_as(p))
+        return tuple(out)
+
+
 class _StackFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, stack, want_all, x, *params):

@@ -78,6 +78,45 @@ def stack_vjp(stack, x, g_out, g_ld, all_grads, need_dx, blob=None):
     return dx, _split(stack, grads)
 
 
+def stack_vjp_inverse(stack, z, g_out, g_ld, all_grads, need_dz, blob=None):
+    """(dz or None, [grad per parameter]) of the INVERSE transform for the
+    upstream gradients of (x_all if all_grads else x_final, log-det)
+    (cnf_vjp_inverse, include/cnf.h)."""
+    z = z.contiguous()
+    B = z.shape[0]
+    dev = z.device
+    if blob is None:
+        blob = stack.prepared(dev)
+    lib = _lib.lib()
+    n = ctypes.c_size_t()
+    _lib.check("cnf_vjp_inverse_workspace_bytes",
+               lib.cnf_vjp_inverse_workspace_bytes(ctypes.byref(stack.desc), ctypes.c_int64(B),
+                                                   ctypes.byref(n)))
+    key = ("inv",) + _stream_key(dev)
+    ws = _ws_cache.get(key)
+    if ws is None or ws.numel() < n.value:
+        ws = torch.empty(max(n.value, 16), dtype=torch.uint8, device=dev)
+        _ws_cache[key] = ws
+    grads = torch.empty(stack.param_count(), dtype=torch.float32, device=dev)
+    dz = torch.empty_like(z) if need_dz else None
+    gx = gxa = None
+    if g_out is not None:
+        g_out = g_out.contiguous().float()
+        if all_grads:
+            gxa = g_out
+        else:
+            gx = g_out
+    gld = g_ld.contiguous().float().reshape(-1) if g_ld is not None else None
+    if gld is not None and gld.numel() == 1 and B != 1:
+        gld = gld.expand(B).contiguous()
+    st = lib.cnf_vjp_inverse(ctypes.byref(stack.desc), _ptr(blob), _ptr(z), _ptr(gx), _ptr(gxa),
+                             _ptr(gld), _ptr(grads), _ptr(dz), ctypes.c_int64(B), _ptr(ws),
+                             ctypes.c_size_t(n.value), _stream(dev))
+    _lib.check("cnf_vjp_inverse", st)
+    stats["vjp"] += 1
+    return dz, _split(stack, grads)
+
+
 def loss_and_grads(stack, x, y, kind=_lib.LOSS_CAL, det=1.0, grad_scale=1.0, need_dx=False):
     """Fused forward + loss + reverse mode.  Returns (terms[3], flat grads, dx)
     where terms = (sum of per-row loss, sum of ce, sum of log-det) over THIS

@@ -285,6 +285,27 @@ int cnf_loss_vjp(const cnf_desc* desc, const void* prepared, const float* x, con
                  loss_terms, grads, dx, B, workspace, workspace_bytes, (hipStream_t)stream);
 }
 
+int cnf_vjp_inverse_workspace_bytes(const cnf_desc* desc, int64_t B, size_t* bytes) {
+  Shape s;
+  int st = derive_shape(desc, &s);
+  if (st != CNF_OK) return st;
+  if (!bytes) return CNF_ERR_NULL;
+  if (B < 0) return CNF_ERR_BATCH;
+  return wvjp_workspace(s, B, bytes);
+}
+
+int cnf_vjp_inverse(const cnf_desc* desc, const void* prepared, const float* z, const float* gx,
+                    const float* gx_all, const float* gld, float* grads, float* dz, int64_t B,
+                    void* workspace, size_t workspace_bytes, void* stream) {
+  Shape s;
+  int st = derive_shape(desc, &s);
+  if (st != CNF_OK) return st;
+  if (B < 0) return CNF_ERR_BATCH;
+  if (!prepared || !grads || (B > 0 && !z)) return CNF_ERR_NULL;
+  return wvjp_inv_run(s, prepared, z, gx, gx_all, gld, grads, dz, B, workspace, workspace_bytes,
+                      (hipStream_t)stream);
+}
+
 const char* cnf_kernel_name(const cnf_desc* desc) {
   Shape s;
   if (derive_shape(desc, &s) != CNF_OK) return "unsupported";

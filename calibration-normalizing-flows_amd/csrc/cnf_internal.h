@@ -111,6 +111,11 @@ int wvjp_run(const Shape& s, const void* prepared, const float* x, const int64_t
              float grad_scale, float* loss_terms, float* grads, float* dx, int64_t B, void* ws,
              size_t ws_bytes, hipStream_t st);
 
+// reverse mode of the INVERSE transform (Flow.backward under autograd)
+int wvjp_inv_run(const Shape& s, const void* prepared, const float* z, const float* gx,
+                 const float* gx_all, const float* gld, float* grads, float* dz, int64_t B,
+                 void* ws, size_t ws_bytes, hipStream_t st);
+
 int vjp_workspace(const Shape& s, int64_t B, size_t* bytes);
 bool vjp2_ok(const Shape& s);  // the packed-pair SGPR reverse-mode kernel serves this shape
 // kind < 0: generic VJP from gz / gz_all / gld;  kind = CNF_LOSS_*: fused loss

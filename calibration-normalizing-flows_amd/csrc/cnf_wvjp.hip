@@ -515,6 +515,102 @@ __global__ __launch_bounds__(256) void k_wbwd_update(
   }
 }
 
+// ---- the inverse transform's reverse mode (wvjp_inv_run) ----
+
+// z natural -> stash layout of the first inverse step's gathered input
+// z'[j] = z[iq[j]] (flip and rev_perm undone, flows/flows.py:115-117)
+__global__ __launch_bounds__(256) void k_winv_stash(const float* __restrict__ z,
+                                                    const int32_t* __restrict__ iq,
+                                                    float* __restrict__ xs, int64_t B, Geo g) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < B; r += nw) {
+    for (int j = lane; j < g.D; j += 64) xs[r * g.Dp + g.col(j)] = z[r * g.D + iq[j]];
+    for (int c = g.DC + lane; c < g.Cp; c += 64) xs[r * g.Dp + c] = c == g.DC ? 1.f : 0.f;
+    for (int c = g.Cp + g.DT + lane; c < g.Dp; c += 64) xs[r * g.Dp + c] = 0.f;
+  }
+}
+
+// One inverse step (flows/flows.py:118-126): x_T = (z'_T - t) e^{-s}, x_C = z'_C;
+// written straight into the next step's gathered stash slot (x[iq_next[j]]).
+__global__ __launch_bounds__(256) void k_winv_fwd_update(const float* __restrict__ X,
+                                                         float* __restrict__ Xn,
+                                                         const float* __restrict__ Os,
+                                                         const float* __restrict__ Ot,
+                                                         const int32_t* __restrict__ iqn,
+                                                         int64_t B, Geo g) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < B; r += nw) {
+    const float* xr = X + r * g.Dp;
+    float* zr = Xn + r * g.Dp;
+    for (int j = lane; j < g.D; j += 64) {
+      const int i = iqn[j];  // next step's z'[j] = this step's x[i]
+      float v = xr[g.col(i)];
+      if (i < g.DT) {
+        const float s = Os ? Os[r * g.DTp + i] : 0.f;
+        const float t = Ot ? Ot[r * g.DTp + i] : 0.f;
+        v = __fmul_rn(__fsub_rn(v, t), expf(-s));
+      }
+      zr[g.col(j)] = v;
+    }
+    for (int c = g.DC + lane; c < g.Cp; c += 64) zr[c] = c == g.DC ? 1.f : 0.f;
+    for (int c = g.Cp + g.DT + lane; c < g.Dp; c += 64) zr[c] = 0.f;
+  }
+}
+
+// Back through one inverse step's coupling: g (natural, this step's output) ->
+// tmp (gathered order z'), G_s / G_t for the conditioners.
+__global__ __launch_bounds__(256) void k_winv_bwd_update(
+    const float* __restrict__ gout, float* __restrict__ tmp, const float* __restrict__ X,
+    const float* __restrict__ Os, const float* __restrict__ Ot, const float* __restrict__ gld,
+    float* __restrict__ Gs, float* __restrict__ Gt, int64_t B, Geo g) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  const int D = g.D, DT = g.DT, DTp = g.DTp;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < B; r += nw) {
+    const float gl = gld[r];
+    for (int j = lane; j < D; j += 64) {
+      const float v = gout[r * D + j];
+      float gz = v;
+      if (j < DT) {
+        const float s = Os ? Os[r * DTp + j] : 0.f;
+        const float t = Ot ? Ot[r * DTp + j] : 0.f;
+        const float e = expf(-s);
+        const float xT = __fmul_rn(__fsub_rn(X[r * g.Dp + g.Cp + j], t), e);
+        gz = __fmul_rn(v, e);
+        if (Gs) Gs[r * DTp + j] = __fsub_rn(-__fmul_rn(v, xT), gl);
+        if (Gt) Gt[r * DTp + j] = -gz;
+      }
+      tmp[r * D + j] = gz;
+    }
+    for (int i = DT + lane; i < DTp; i += 64) {
+      if (Gs) Gs[r * DTp + i] = 0.f;
+      if (Gt) Gt[r * DTp + i] = 0.f;
+    }
+  }
+}
+
+// g_{z_in}[iq[j]] = tmp[j] (+ the caller's gradient of that output); skip: no
+// destination wanted (dz == NULL on the last step)
+__global__ __launch_bounds__(256) void k_winv_scatter(const float* __restrict__ tmp,
+                                                      float* __restrict__ out,
+                                                      const float* __restrict__ gprev,
+                                                      const int32_t* __restrict__ iq, int64_t B,
+                                                      int D, int skip) {
+  if (skip) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < B; r += nw) {
+    for (int j = lane; j < D; j += 64) {
+      const int i = iq[j];
+      float v = tmp[r * D + j];
+      if (gprev) v += gprev[r * D + i];
+      out[r * D + i] = v;
+    }
+  }
+}
+
 inline int64_t al64(int64_t floats) { return (floats + 63) / 64 * 64; }
 
 int lin_out(const Shape& s, int k) { return k == s.n_lin - 1 ? s.DT : s.units[k + 1]; }
@@ -667,145 +763,131 @@ int wvjp_workspace(const Shape& s, int64_t B, size_t* bytes) {
   return CNF_OK;
 }
 
-int wvjp_run(const Shape& s, const void* prepared, const float* x, const int64_t* y,
-             const float* gz, const float* gz_all, const float* gld_in, int kind, float det,
-             float grad_scale, float* loss_terms, float* grads, float* dx, int64_t B, void* ws,
-             size_t ws_bytes, hipStream_t st) {
-  if (!wvjp_ok(s)) return CNF_ERR_UNSUPPORTED;
-  const Plan p = make_plan(s, B);
-  if (!ws || ws_bytes < (size_t)p.total * 4) return CNF_ERR_NULL;
-  const int64_t P = s.layer_floats * s.L;
-  if (B == 0) {
-    if (P > 0 && hipMemsetAsync(grads, 0, (size_t)P * 4, st) != hipSuccess) return check_launch();
-    if (loss_terms && hipMemsetAsync(loss_terms, 0, 3 * 4, st) != hipSuccess) return check_launch();
-    return check_launch();
-  }
-  float* W = static_cast<float*>(ws);
-  const char* base = static_cast<const char*>(prepared);
-  const int32_t* fq = reinterpret_cast<const int32_t*>(base);
-  const float* plain = reinterpret_cast<const float*>(base + idx_bytes(s)) + s.plain_region;
-  const Geo geom = geo(s);
-  const int D = s.D, DT = s.DT, DC = s.DC, NL = s.n_lin, L = s.L;
-  const int64_t PL = s.layer_floats, PS = al64(PL), Dp = geom.Dp;
-  float* ld = W + p.ld;
-  float* gld = W + p.gld;
-  float* part = W + p.part;
-  auto Xs = [&](int l) { return W + p.stash + (int64_t)l * B * Dp; };  // input of layer l
-  auto wptr = [&](int l, int n, int k) { return plain + l * PL + n * s.net_floats + lin_off(s, k); };
-  auto bptr = [&](int l, int n, int k) {
-    return wptr(l, n, k) + (int64_t)s.units[k + 1] * s.units[k];
-  };
-  const unsigned wave_blocks = (unsigned)std::min<int64_t>((B + 3) / 4, 16384);
+namespace {
 
-  // conditioner forward of layer l from its stashed input: H[n][k], O[n]
-  // layer l's conditioner activations (one shared set unless keep_acts)
-  auto Hb = [&](int l, int n, int k) { return W + p.H[n][k] + (int64_t)l * p.act_stride; };
-  auto Ob = [&](int l, int n) { return W + p.O[n] + (int64_t)l * p.act_stride; };
-  auto nets_forward = [&](int l) {
+// Host side of one layer-at-a-time sweep: workspace views and the per-layer
+// launch sequences shared by the forward transform's reverse mode (wvjp_run)
+// and the inverse transform's (wvjp_inv_run).  A "slot" indexes the stashed
+// inputs / kept activations in sweep order, a "layer" the parameters.
+struct Runner {
+  const Shape& s;
+  const Plan& p;
+  float* W;
+  const float* plain;
+  Geo geom;
+  int64_t B;
+  hipStream_t st;
+  int D, DT, DC, NL, L;
+  int64_t PL, PS, Dp;
+  unsigned wave_blocks;
+  int dw_calls = 0;
+
+  Runner(const Shape& s_, const Plan& p_, void* ws, const void* prepared, int64_t B_,
+         hipStream_t st_)
+      : s(s_), p(p_), W(static_cast<float*>(ws)),
+        plain(reinterpret_cast<const float*>(static_cast<const char*>(prepared) + idx_bytes(s_)) +
+              s_.plain_region),
+        geom(geo(s_)), B(B_), st(st_), D(s_.D), DT(s_.DT), DC(s_.DC), NL(s_.n_lin), L(s_.L),
+        PL(s_.layer_floats), PS(al64(s_.layer_floats)), Dp(geo(s_).Dp),
+        wave_blocks((unsigned)std::min<int64_t>((B_ + 3) / 4, 16384)) {}
+
+  float* Xs(int slot) const { return W + p.stash + (int64_t)slot * B * Dp; }
+  float* Hb(int slot, int n, int k) const {
+    return W + p.H[n][k] + (int64_t)slot * p.act_stride;
+  }
+  float* Ob(int slot, int n) const { return W + p.O[n] + (int64_t)slot * p.act_stride; }
+  const float* Os(int slot) const { return s.scale ? Ob(slot, 0) : nullptr; }
+  const float* Ot(int slot) const { return s.shift ? Ob(slot, s.scale) : nullptr; }
+  float* Gk(int n, int k) const { return W + p.G[n][k]; }
+  const float* wptr(int layer, int n, int k) const {
+    return plain + layer * PL + n * s.net_floats + lin_off(s, k);
+  }
+  const float* bptr(int layer, int n, int k) const {
+    return wptr(layer, n, k) + (int64_t)s.units[k + 1] * s.units[k];
+  }
+  int act(int n) const { return (s.s_tanh && s.scale && n == 0) ? 2 : 1; }
+
+  // both conditioners of `layer` on the conditioning half of slot `slot`
+  void nets_forward(int slot, int layer) const {
     for (int k = 0; k < NL; ++k) {
       GemmArgs ga{};
       ga.M = B;
       const bool last = k == NL - 1;
       for (int n = 0; n < s.nets; ++n) {
         GemmJob& j = ga.job[n];
-        j.A = k == 0 ? Xs(l) : Hb(l, n, k - 1);
+        j.A = k == 0 ? Xs(slot) : Hb(slot, n, k - 1);
         j.lda = k == 0 ? Dp : hp(s, k - 1);
         j.K = lin_in(s, k);
-        j.Bw = wptr(l, n, k) + (k == 0 ? DT : 0);
+        j.Bw = wptr(layer, n, k) + (k == 0 ? DT : 0);
         j.ldb = s.units[k];
         j.N = lin_out(s, k);
-        j.bias = bptr(l, n, k);
-        j.C = last ? Ob(l, n) : Hb(l, n, k);
+        j.bias = bptr(layer, n, k);
+        j.C = last ? Ob(slot, n) : Hb(slot, n, k);
         j.ldc = last ? geom.DTp : hp(s, k);
         j.ldw = last ? j.N : hp(s, k);
         j.ones = !last;
-        j.act = (s.s_tanh && s.scale && n == 0) ? 2 : 1;
+        j.act = act(n);
       }
       gemm(ga, B, ga.job[0].ldw, lin_in(s, k), s.nets, true, last ? kEpiBias : kEpiBiasRelu,
            false, st);
     }
-  };
-  auto Os = [&](int l) -> const float* { return s.scale ? Ob(l, 0) : nullptr; };
-  auto Ot = [&](int l) -> const float* { return s.shift ? Ob(l, s.scale) : nullptr; };
-
-  // ---- forward sweep ----
-  hipLaunchKernelGGL(k_wstash, dim3(wave_blocks), dim3(256), 0, st, x, Xs(0), B, geom);
-  for (int l = 0; l < L; ++l) {
-    if (s.nets) nets_forward(l);
-    hipLaunchKernelGGL(k_wfwd_update, dim3(wave_blocks), dim3(256), 0, st, Xs(l), Xs(l + 1), ld,
-                       Os(l), Ot(l), fq + l * D, B, geom, l == 0);
   }
-  // ---- seed ----
-  float* g[2] = {W + p.g0, W + p.g1};
-  int cur = 0;
-  hipLaunchKernelGGL(k_wseed, dim3((unsigned)p.nseed), dim3(256), 0, st, Xs(L), ld, y, kind, det,
-                     grad_scale, gz, gz_all ? gz_all + (int64_t)(L - 1) * B * D : nullptr, gld_in,
-                     g[0], gld, W + p.seed, B, geom);
-  if (kind >= 0) reduce_partials(W + p.seed, (int)p.nseed, 4, 0, nullptr, loss_terms, st);
-  if (P > 0 && hipMemsetAsync(part, 0, (size_t)p.nkb * PS * 4, st) != hipSuccess)
-    return check_launch();
 
-  // ---- backward sweep ----
-  for (int l = L - 1; l >= 0; --l) {
-    if (s.nets && !p.keep_acts) nets_forward(l);  // recompute, or the kept activations
-    float* gin = (l == 0 && dx) ? dx : g[cur ^ 1];
-    float* Gs = s.scale ? W + p.G[0][NL - 1] : nullptr;
-    float* Gt = s.shift ? W + p.G[s.scale][NL - 1] : nullptr;
-    hipLaunchKernelGGL(k_wbwd_update, dim3(wave_blocks), dim3(256), 0, st, g[cur], gin, Xs(l), Os(l),
-                       gld, Gs, Gt, gz_all && l > 0 ? gz_all + (int64_t)(l - 1) * B * D : nullptr,
-                       fq + l * D, B, geom);
-    if (s.nets == 0) {
-      cur ^= 1;
-      continue;
-    }
-    for (int k = NL - 1; k >= 1; --k) {  // G_{k-1} = (G_k W_k) * relu'(H_{k-1})
+  // back through both conditioners from their output gradients Gk(n, NL-1):
+  // G_{k-1} = (G_k W_k) * act'(H_{k-1}), then gin[:, DT:] += sum_n G_0 W_0[:, DT:]
+  void nets_backward(int slot, int layer, float* gin) const {
+    for (int k = NL - 1; k >= 1; --k) {
       GemmArgs ga{};
       ga.M = B;
       for (int n = 0; n < s.nets; ++n) {
         GemmJob& j = ga.job[n];
-        j.A = W + p.G[n][k];
+        j.A = Gk(n, k);
         j.lda = gp(s, k);
         j.K = lin_out(s, k);
-        j.Bw = wptr(l, n, k);
+        j.Bw = wptr(layer, n, k);
         j.ldb = s.units[k];
         j.N = s.units[k];
-        j.C = W + p.G[n][k - 1];
+        j.C = Gk(n, k - 1);
         j.ldc = gp(s, k - 1);
         j.ldw = gp(s, k - 1);
-        j.mask = Hb(l, n, k - 1);
+        j.mask = Hb(slot, n, k - 1);
         j.ldm = hp(s, k - 1);
-        j.act = (s.s_tanh && s.scale && n == 0) ? 2 : 1;
+        j.act = act(n);
       }
       gemm(ga, B, gp(s, k - 1), lin_out(s, k), s.nets, false, kEpiMask, false, st);
     }
-    {  // g_in[:, DT:] += sum over nets of G_0 W_0[:, DT:]
-      GemmArgs ga{};
-      ga.M = B;
-      GemmJob& j = ga.job[0];
-      j.A = W + p.G[0][0];
-      j.lda = gp(s, 0);
-      j.K = lin_out(s, 0);
-      j.Bw = wptr(l, 0, 0) + DT;
-      j.ldb = D;
-      if (s.nets == 2) {
-        j.A2 = W + p.G[1][0];
-        j.lda2 = j.lda;
-        j.Bw2 = wptr(l, 1, 0) + DT;
-        j.ldb2 = D;
-      }
-      j.N = DC;
-      j.C = gin + DT;
-      j.ldc = D;
-      j.ldw = DC;
-      gemm(ga, B, DC, j.K, 1, false, kEpiAdd, s.nets == 2, st);
+    GemmArgs ga{};
+    ga.M = B;
+    GemmJob& j = ga.job[0];
+    j.A = Gk(0, 0);
+    j.lda = gp(s, 0);
+    j.K = lin_out(s, 0);
+    j.Bw = wptr(layer, 0, 0) + DT;
+    j.ldb = D;
+    if (s.nets == 2) {
+      j.A2 = Gk(1, 0);
+      j.lda2 = j.lda;
+      j.Bw2 = wptr(layer, 1, 0) + DT;
+      j.ldb2 = D;
     }
-    // weight / bias gradients of every Linear of both nets: one launch.  The
-    // partial records are reused across layers: positions a layer never writes
-    // (masked columns / rows) keep the zeros of the memset, except that under
+    j.N = DC;
+    j.C = gin + DT;
+    j.ldc = D;
+    j.ldw = DC;
+    gemm(ga, B, DC, j.K, 1, false, kEpiAdd, s.nets == 2, st);
+  }
+
+  // weight / bias gradients of every Linear of both nets (one launch) into the
+  // per-row-block partials, then their fixed-order sum into grads_layer
+  int weight_grads(int slot, int layer, float* grads_layer) {
+    float* part = W + p.part;
+    // the records are reused across layers: positions a layer never writes
+    // (masked columns / rows) keep the first memset's zeros, except that under
     // the legacy alternate mask odd and even layers mask different positions
-    if (s.alt_mask && l < L - 1 &&
+    if (s.alt_mask && dw_calls > 0 &&
         hipMemsetAsync(part, 0, (size_t)p.nkb * PS * 4, st) != hipSuccess)
       return check_launch();
+    ++dw_calls;
     DwArgs da{};
     da.partials = part;
     da.M = B;
@@ -815,16 +897,16 @@ int wvjp_run(const Shape& s, const void* prepared, const float* x, const int64_t
     for (int n = 0; n < s.nets; ++n) {
       for (int k = 0; k < NL; ++k) {
         DwJob& j = da.job[jobs++];
-        j.G = W + p.G[n][k];
+        j.G = Gk(n, k);
         j.ldg = gp(s, k);
-        j.H = k == 0 ? Xs(l) : Hb(l, n, k - 1);
+        j.H = k == 0 ? Xs(slot) : Hb(slot, n, k - 1);
         j.ldh = k == 0 ? Dp : hp(s, k - 1);
         j.N = lin_out(s, k);
         j.K = lin_in(s, k);
         // legacy alternate mask: an odd layer's kernel weights are its
         // parameters with the first Linear's columns and the last Linear's
         // rows reversed (cnf_tile.hip prepare); map the gradients back
-        const bool rev = s.alt_mask && (l & 1);
+        const bool rev = s.alt_mask && (layer & 1);
         const bool rin = rev && k == 0, rout = rev && k == NL - 1;
         j.cstep = rin ? -1 : 1;
         j.rrev = rout;
@@ -839,8 +921,128 @@ int wvjp_run(const Shape& s, const void* prepared, const float* x, const int64_t
     hipLaunchKernelGGL(k_wdw<kDwCols / 32>,
                        dim3((unsigned)p.nkb, (unsigned)jobs, (unsigned)max_subs), dim3(64), 0, st,
                        da);
-    reduce_partials(part, (int)p.nkb, (int)PS, (int)PL, grads + (int64_t)l * PL, nullptr, st);
+    reduce_partials(part, (int)p.nkb, (int)PS, (int)PL, grads_layer, nullptr, st);
+    return CNF_OK;
+  }
+};
+
+int empty_batch(const Shape& s, float* grads, float* loss_terms, hipStream_t st) {
+  const int64_t P = s.layer_floats * s.L;
+  if (P > 0 && hipMemsetAsync(grads, 0, (size_t)P * 4, st) != hipSuccess) return check_launch();
+  if (loss_terms && hipMemsetAsync(loss_terms, 0, 3 * 4, st) != hipSuccess) return check_launch();
+  return check_launch();
+}
+
+}  // namespace
+
+int wvjp_run(const Shape& s, const void* prepared, const float* x, const int64_t* y,
+             const float* gz, const float* gz_all, const float* gld_in, int kind, float det,
+             float grad_scale, float* loss_terms, float* grads, float* dx, int64_t B, void* ws,
+             size_t ws_bytes, hipStream_t st) {
+  if (!wvjp_ok(s)) return CNF_ERR_UNSUPPORTED;
+  const Plan p = make_plan(s, B);
+  if (!ws || ws_bytes < (size_t)p.total * 4) return CNF_ERR_NULL;
+  if (B == 0) return empty_batch(s, grads, loss_terms, st);
+  Runner R(s, p, ws, prepared, B, st);
+  const int32_t* fq = reinterpret_cast<const int32_t*>(prepared);
+  const int D = s.D, NL = s.n_lin, L = s.L;
+  float* W = R.W;
+  float* ld = W + p.ld;
+  float* gld = W + p.gld;
+
+  // ---- forward sweep: slot l = input of layer l ----
+  hipLaunchKernelGGL(k_wstash, dim3(R.wave_blocks), dim3(256), 0, st, x, R.Xs(0), B, R.geom);
+  for (int l = 0; l < L; ++l) {
+    if (s.nets) R.nets_forward(l, l);
+    hipLaunchKernelGGL(k_wfwd_update, dim3(R.wave_blocks), dim3(256), 0, st, R.Xs(l), R.Xs(l + 1),
+                       ld, R.Os(l), R.Ot(l), fq + l * D, B, R.geom, l == 0);
+  }
+  // ---- seed ----
+  float* g[2] = {W + p.g0, W + p.g1};
+  int cur = 0;
+  hipLaunchKernelGGL(k_wseed, dim3((unsigned)p.nseed), dim3(256), 0, st, R.Xs(L), ld, y, kind, det,
+                     grad_scale, gz, gz_all ? gz_all + (int64_t)(L - 1) * B * D : nullptr, gld_in,
+                     g[0], gld, W + p.seed, B, R.geom);
+  if (kind >= 0) reduce_partials(W + p.seed, (int)p.nseed, 4, 0, nullptr, loss_terms, st);
+  if (R.PL > 0 && hipMemsetAsync(W + p.part, 0, (size_t)p.nkb * R.PS * 4, st) != hipSuccess)
+    return check_launch();
+
+  // ---- backward sweep ----
+  for (int l = L - 1; l >= 0; --l) {
+    if (s.nets && !p.keep_acts) R.nets_forward(l, l);  // recompute, or the kept activations
+    float* gin = (l == 0 && dx) ? dx : g[cur ^ 1];
+    float* Gs = s.scale ? R.Gk(0, NL - 1) : nullptr;
+    float* Gt = s.shift ? R.Gk(s.scale, NL - 1) : nullptr;
+    hipLaunchKernelGGL(k_wbwd_update, dim3(R.wave_blocks), dim3(256), 0, st, g[cur], gin, R.Xs(l),
+                       R.Os(l), gld, Gs, Gt,
+                       gz_all && l > 0 ? gz_all + (int64_t)(l - 1) * B * D : nullptr, fq + l * D,
+                       B, R.geom);
+    if (s.nets) {
+      R.nets_backward(l, l, gin);
+      const int r = R.weight_grads(l, l, grads + (int64_t)l * R.PL);
+      if (r != CNF_OK) return r;
+    }
     cur ^= 1;
+  }
+  return check_launch();
+}
+
+// Reverse mode of the INVERSE transform (flows/flows.py:114-126, Flow.backward
+// under autograd): step i runs layer l = L-1-i on z' = z_in[:, iq_l] (flip and
+// rev_perm undone as a gather), x_T = (z'_T - t) e^{-s}, x_C = z'_C,
+// ld -= sum s.  Slot i holds step i's gathered input.  Backward, per step:
+//   g_{z'_T} = g_T e^{-s},  G_t = -g_T e^{-s},  G_s = -g_T x_T - gld,
+//   g_{z'_C} = g_C + (conditioners' share), then g_{z_in}[iq_l[j]] = g_{z'}[j]
+//   plus the caller's gradient of the previous step's output.
+int wvjp_inv_run(const Shape& s, const void* prepared, const float* z, const float* gx,
+                 const float* gx_all, const float* gld_in, float* grads, float* dz, int64_t B,
+                 void* ws, size_t ws_bytes, hipStream_t st) {
+  if (!wvjp_ok(s)) return CNF_ERR_UNSUPPORTED;
+  const Plan p = make_plan(s, B);
+  if (!ws || ws_bytes < (size_t)p.total * 4) return CNF_ERR_NULL;
+  if (B == 0) return empty_batch(s, grads, nullptr, st);
+  Runner R(s, p, ws, prepared, B, st);
+  const int32_t* iq = reinterpret_cast<const int32_t*>(prepared) + s.L * s.D;
+  const int D = s.D, NL = s.n_lin, L = s.L;
+  float* W = R.W;
+  float* gld = W + p.gld;
+
+  // ---- forward sweep (the inverse): slot i = gathered input of step i ----
+  hipLaunchKernelGGL(k_winv_stash, dim3(R.wave_blocks), dim3(256), 0, st, z, iq + (L - 1) * D,
+                     R.Xs(0), B, R.geom);
+  for (int i = 0; i < L; ++i) {
+    const int l = L - 1 - i;
+    if (s.nets) R.nets_forward(i, l);
+    if (i + 1 < L)
+      hipLaunchKernelGGL(k_winv_fwd_update, dim3(R.wave_blocks), dim3(256), 0, st, R.Xs(i),
+                         R.Xs(i + 1), R.Os(i), R.Ot(i), iq + (l - 1) * D, B, R.geom);
+  }
+  // ---- seed: gradient of the last step's output (the flow's input estimate) ----
+  float* g[2] = {W + p.g0, W + p.g1};
+  float* tmp = W + p.g0;  // reuse: g ping-pongs between g1 and tmp below
+  hipLaunchKernelGGL(k_wseed, dim3((unsigned)p.nseed), dim3(256), 0, st, R.Xs(0), gld, nullptr,
+                     -1, 0.f, 1.f, gx, gx_all ? gx_all + (int64_t)(L - 1) * B * D : nullptr,
+                     gld_in, g[1], gld, W + p.seed, B, R.geom);
+  if (R.PL > 0 && hipMemsetAsync(W + p.part, 0, (size_t)p.nkb * R.PS * 4, st) != hipSuccess)
+    return check_launch();
+
+  // ---- backward sweep over the steps, last first ----
+  for (int i = L - 1; i >= 0; --i) {
+    const int l = L - 1 - i;
+    if (s.nets && !p.keep_acts) R.nets_forward(i, l);
+    float* Gs = s.scale ? R.Gk(0, NL - 1) : nullptr;
+    float* Gt = s.shift ? R.Gk(s.scale, NL - 1) : nullptr;
+    hipLaunchKernelGGL(k_winv_bwd_update, dim3(R.wave_blocks), dim3(256), 0, st, g[1], tmp,
+                       R.Xs(i), R.Os(i), R.Ot(i), gld, Gs, Gt, B, R.geom);
+    if (s.nets) {
+      R.nets_backward(i, l, tmp);
+      const int r = R.weight_grads(i, l, grads + (int64_t)l * R.PL);
+      if (r != CNF_OK) return r;
+    }
+    hipLaunchKernelGGL(k_winv_scatter, dim3(R.wave_blocks), dim3(256), 0, st, tmp,
+                       i == 0 ? dz : g[1],
+                       gx_all && i > 0 ? gx_all + (int64_t)(i - 1) * B * D : nullptr,
+                       iq + l * D, B, D, i == 0 && dz == nullptr);
   }
   return check_launch();
 }

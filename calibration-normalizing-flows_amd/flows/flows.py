@@ -132,11 +132,13 @@ class Flow(nn.Module):
         stack = self._native_stack()
         try:
             if torch.is_grad_enabled() and (x.requires_grad or stack.requires_grad()):
-                if inverse:
-                    # no native reverse mode of the inverse: the reference's ops
-                    _not_native("autograd through the inverse (Flow.backward)")
-                    return None
-                out, ld = stack.forward_autograd(x, want_all=want_all)
+                if inverse:  # cnf_vjp_inverse
+                    if stack.strict_nan:
+                        _not_native("autograd through the strict-NaN inverse")
+                        return None
+                    out, ld = stack.inverse_autograd(x, want_all=want_all)
+                else:
+                    out, ld = stack.forward_autograd(x, want_all=want_all)
             else:
                 fin, ld, allt = stack.run(x, inverse=inverse, want_all=want_all)
                 out = allt if want_all else fin
@@ -265,10 +267,13 @@ class NvpCouplingLayer(nn.Module):
             self._stack = CouplingStack([self], strict_nan=strict)
         try:
             if _needs_grad(x, self):
-                if inverse:
-                    _not_native("autograd through the inverse (NvpCouplingLayer.backward)")
-                    return None
-                z, ld = self._stack.forward_autograd(x, want_all=False)
+                if inverse:  # cnf_vjp_inverse
+                    if strict:
+                        _not_native("autograd through the strict-NaN inverse")
+                        return None
+                    z, ld = self._stack.inverse_autograd(x, want_all=False)
+                else:
+                    z, ld = self._stack.forward_autograd(x, want_all=False)
             else:
                 z, ld, _ = self._stack.run(x, inverse=inverse)
             return z, _squeeze_ld(ld)

@@ -129,9 +129,11 @@ class LegacyRealNvpFlow(nn.Module):
         return x, ld
 
     def backward(self, y):
-        if self._native_ok(y) and not (torch.is_grad_enabled() and
-                                       (y.requires_grad or self._native_stack().requires_grad())):
-            x, ld, _ = self._native_stack().run(y, inverse=True)
+        if self._native_ok(y):
+            stack = self._native_stack()
+            if torch.is_grad_enabled() and (y.requires_grad or stack.requires_grad()):
+                return stack.inverse_autograd(y, want_all=False)  # cnf_vjp_inverse
+            x, ld, _ = stack.run(y, inverse=True)
             return x, ld
         ld = torch.zeros(y.shape[0], dtype=y.dtype, device=y.device)
         for ly in reversed(self.layers):

@@ -178,6 +178,20 @@ int cnf_loss_vjp(const cnf_desc* desc, const void* prepared, const float* x,
  * shapes whose Linears exceed 32 floats, misaligned views), "mfma-wide"
  * (register-resident MFMA, the wide shapes of its table), "mfma-tile" (other
  * wide shapes, every-layer outputs of wide stacks). */
+/* Reverse mode of cnf_inverse (autograd through Flow.backward, flows/flows.py:
+ * 27-37 / 114-126): given upstream gradients of the inverse's outputs, writes
+ *   grads  [cnf_param_count]  d/d(parameters), state_dict order (overwritten)
+ *   dz     [B][D]             d/dz, may be NULL
+ * Upstream inputs, each may be NULL (= zero):
+ *   gx     [B][D]     gradient of the final output (xs[-1], the input estimate)
+ *   gx_all [L][B][D]  gradient of every step's output (the xs list, step order)
+ *   gld    [B]        gradient of the inverse's per-sample log-det
+ * Layer-at-a-time MFMA reverse mode for every shape (non-strict). */
+int cnf_vjp_inverse_workspace_bytes(const cnf_desc* desc, int64_t B, size_t* bytes);
+int cnf_vjp_inverse(const cnf_desc* desc, const void* prepared, const float* z, const float* gx,
+                    const float* gx_all, const float* gld, float* grads, float* dz, int64_t B,
+                    void* workspace, size_t workspace_bytes, void* stream);
+
 /* One Adam step over every parameter (torch.optim.Adam's update, amsgrad off;
  * the optimizer of TorchFlowCalibrator.fit, calibrators.py:239-295) in one
  * launch, fed by the flat gradient of cnf_loss_vjp / cnf_vjp:
