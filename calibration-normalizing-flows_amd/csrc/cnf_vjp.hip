@@ -35,6 +35,7 @@
 #include "cnf_valu_common.h"
 #include "cnf_sgpr_common.h"
 #include "cnf_valu_io.h"
+#include "cnf_vjp2.h"
 
 namespace cnf {
 namespace {
@@ -60,11 +61,7 @@ struct VS {
                                        : H1 * D + H1 + H2 * H1 + H2 + D * H2 + D;
 };
 
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
+using v2::wave_sync;  // cnf_vjp2.h
 
 // One MLP forward keeping its activations (compact weights, cnf_valu_common.h).
 template <int D, int H1, int H2>
@@ -552,561 +549,6 @@ __global__ __launch_bounds__(kRR) void k_reduce_rows4(const float4* __restrict__
   }
 }
 
-// ===========================================================================
-// k_vjp2: reverse mode on packed row pairs (two rows per lane, v_pk_fma_f32)
-// with the weights as SGPR operands (the plain packed-SGPR region), for the
-// narrow shapes whose conditioner gradient stacks fit one 16x16 MFMA tile
-// (GS = H1 + H2 + D/2 <= 16, HS = D - D/2 + H1 + H2 + 1 <= 16) and L <= 8.
-//
-// One wave per block walks tiles of 128 rows (grid-strided):
-//   forward   the L layers, each layer's transformed-half input x_T stashed
-//             in the workspace (HBM scratch, written and re-read by the same
-//             wave within the tile: L2-resident in practice);
-//   seed      the loss gradient (or gz / gld / gz_all of a generic VJP);
-//   backward  per layer, last to first: undo flip / perm (renaming), recompute
-//             both conditioners on the conditioning half, take the layer's
-//             input x_T from the stash (recovering it as (z_T - t) exp(-s)
-//             loses the reference's precision once |s| is large), back-
-//             propagate through the affine update
-//             and both MLPs (transposed products on SGPR weights);
-//   dW        each net's G = [g_a1, g_a2, g_out] and H = [c, h1, h2, 1] go
-//             through a 16 KB LDS stage 64 rows at a time and are folded into a
-//             16x16 accumulator by v_mfma_f32_16x16x4f32 with the rows as K;
-//             the accumulators of all (layer, net) live in registers for the
-//             wave's whole run and are written once, as this wave's partial.
-// Partials are summed in wave order by k_reduce_cols (deterministic).
-// ===========================================================================
-template <int I, int N, class F>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (I < N) {
-    f(std::integral_constant<int, I>{});
-    static_for<I + 1, N>(f);
-  }
-}
-
-constexpr int kV2TR = 128;   // rows per wave tile (lane l: rows 2l, 2l+1)
-constexpr int kV2LMax = 8;   // layers the register accumulators hold
-constexpr int kV2SS = 68;    // stage row stride in floats (64 rows + pad, 16-B aligned)
-
-struct VArgs2 {
-  const float* x;
-  const int64_t* y;
-  const float* gz;
-  const float* gz_all;
-  const float* gld;
-  float* dx;
-  float* partials;
-  float* stash;  // [L][B][D/2] transformed-half layer inputs
-  int64_t B;
-  int L, kind;
-  float det, grad_scale;
-  int P, PS;
-};
-
-// widx: W[o][k] in the packed row layout [w_o0, b_o, w_o1 .. ] at stride S
-template <int S>
-__device__ __forceinline__ constexpr int widx(int o, int k) { return o * S + (k == 0 ? 0 : 1 + k); }
-
-// y[o] = b[o] + sum_k W[o][k] x[k], o < NOUT (plain weights; input-major chains)
-template <int NIN, int NOUT, int S, bool RELU, int NC>
-__device__ __forceinline__ void vlin(const SW<NC>& w, const f2* x, f2* y) {
-  f2 a[NOUT];
-#pragma unroll
-  for (int o = 0; o < NOUT; ++o) a[o] = fma_wb(w.pair(o * S), x[0]);
-#pragma unroll
-  for (int k = 1; k < NIN; ++k)
-#pragma unroll
-    for (int o = 0; o < NOUT; ++o) a[o] = fmaT(w[widx<S>(o, k)], x[k], a[o]);
-#pragma unroll
-  for (int o = 0; o < NOUT; ++o) y[o] = RELU ? maxT(a[o], splat(0.f, f2{})) : a[o];
-}
-
-// gin[k] = sum_o W[o][k] gout[o], k < NIN, o < NOUT
-template <int NIN, int NOUT, int S, int NC>
-__device__ __forceinline__ void vlin_t(const SW<NC>& w, const f2* gout, f2* gin) {
-#pragma unroll
-  for (int k = 0; k < NIN; ++k) gin[k] = gout[0] * splat(w[widx<S>(0, k)], f2{});
-#pragma unroll
-  for (int o = 1; o < NOUT; ++o)
-#pragma unroll
-    for (int k = 0; k < NIN; ++k) gin[k] = fmaT(w[widx<S>(o, k)], gout[o], gin[k]);
-}
-
-template <int NC>
-__device__ __forceinline__ void sload_now(SW<NC>& w, const float* p) {
-  sissue(w, p);
-  sready();
-}
-
-// One net's activations on the conditioning half c (plain weights): h1, h2, out.
-template <class S, int NC>
-__device__ __forceinline__ void vnet_fwd(const float* wn, const f2* c, f2* h1, f2* h2, f2* out) {
-  SW<NC> w;
-  if constexpr (S::NL == 1) {
-    sload_now(w, wn);
-    vlin<S::nin(0), S::nout(0), S::stride(0), false>(w, c, out);
-  } else if constexpr (S::NL == 2) {
-    sload_now(w, wn);
-    vlin<S::nin(0), S::nout(0), S::stride(0), true>(w, c, h1);
-    sload_now(w, wn + S::off(1));
-    vlin<S::nin(1), S::nout(1), S::stride(1), false>(w, h1, out);
-  } else {
-    sload_now(w, wn);
-    vlin<S::nin(0), S::nout(0), S::stride(0), true>(w, c, h1);
-    sload_now(w, wn + S::off(1));
-    vlin<S::nin(1), S::nout(1), S::stride(1), true>(w, h1, h2);
-    sload_now(w, wn + S::off(2));
-    vlin<S::nin(2), S::nout(2), S::stride(2), false>(w, h2, out);
-  }
-}
-
-// Back-propagate one net: gout (d/d out) -> adds d/dc into gc and leaves the
-// gradient stack G = [g_a1, g_a2, gout] (pre-activation gradients).
-template <class S, int NC>
-__device__ __forceinline__ void vnet_bwd(const float* wn, const f2* h1, const f2* h2,
-                                         const f2* gout, f2* gc, f2* G) {
-  constexpr int H1 = S::NL >= 2 ? S::nout(0) : 0, H2 = S::NL == 3 ? S::nout(1) : 0;
-  constexpr int DT = S::DT, DC = S::DC;
-  SW<NC> w;
-  f2 gin[DC];
-  const f2 zero = splat(0.f, f2{});
-  if constexpr (S::NL == 1) {
-    sload_now(w, wn);
-    vlin_t<DC, DT, S::stride(0)>(w, gout, gin);
-  } else if constexpr (S::NL == 2) {
-    f2 g1[H1];
-    sload_now(w, wn + S::off(1));
-    vlin_t<H1, DT, S::stride(1)>(w, gout, g1);
-#pragma unroll
-    for (int m = 0; m < H1; ++m) {
-      const f2 h = h1[m];
-      g1[m] = f2{h.x > 0.f ? g1[m].x : 0.f, h.y > 0.f ? g1[m].y : 0.f};
-      G[m] = g1[m];
-    }
-    sload_now(w, wn);
-    vlin_t<DC, H1, S::stride(0)>(w, g1, gin);
-  } else {
-    f2 g2[H2], g1[H1];
-    sload_now(w, wn + S::off(2));
-    vlin_t<H2, DT, S::stride(2)>(w, gout, g2);
-#pragma unroll
-    for (int m = 0; m < H2; ++m) {
-      const f2 h = h2[m];
-      g2[m] = f2{h.x > 0.f ? g2[m].x : 0.f, h.y > 0.f ? g2[m].y : 0.f};
-      G[H1 + m] = g2[m];
-    }
-    sload_now(w, wn + S::off(1));
-    vlin_t<H1, H2, S::stride(1)>(w, g2, g1);
-#pragma unroll
-    for (int m = 0; m < H1; ++m) {
-      const f2 h = h1[m];
-      g1[m] = f2{h.x > 0.f ? g1[m].x : 0.f, h.y > 0.f ? g1[m].y : 0.f};
-      G[m] = g1[m];
-    }
-    sload_now(w, wn);
-    vlin_t<DC, H1, S::stride(0)>(w, g1, gin);
-  }
-#pragma unroll
-  for (int j = 0; j < DT; ++j) G[H1 + H2 + j] = gout[j];
-#pragma unroll
-  for (int k = 0; k < DC; ++k) gc[k] += gin[k];
-  (void)zero;
-}
-
-// Fold G^T H of this tile's 128 rows (GS x HS <= 16 x 16) into acc: the stage
-// holds 64 rows at a time ([feature][row], G features 0..15 then H 16..31);
-// lane l feeds MFMA step ks with feature l%16 of row (l/16)*16 + ks, so its
-// operands for all 16 steps are 16 contiguous floats (4 ds_read_b128).
-template <int GS, int HS>
-__device__ __forceinline__ floatx4 wgrad_tile(float* st, const f2* G, const f2* H, int lane,
-                                              floatx4 acc) {
-#pragma unroll
-  for (int ch = 0; ch < 2; ++ch) {
-    wave_sync();  // the previous reads of the stage are done
-#pragma unroll
-    for (int f = 0; f < GS; ++f) st[f * kV2SS + lane] = ch ? G[f].y : G[f].x;
-#pragma unroll
-    for (int f = 0; f < HS; ++f) st[(16 + f) * kV2SS + lane] = ch ? H[f].y : H[f].x;
-    wave_sync();
-    const float4* ga = reinterpret_cast<const float4*>(st + (lane & 15) * kV2SS + (lane >> 4) * 16);
-    const float4* hb =
-        reinterpret_cast<const float4*>(st + (16 + (lane & 15)) * kV2SS + (lane >> 4) * 16);
-    float4 A[4], Bv[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      A[q] = ga[q];
-      Bv[q] = hb[q];
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(A[q].x, Bv[q].x, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(A[q].y, Bv[q].y, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(A[q].z, Bv[q].z, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(A[q].w, Bv[q].w, acc, 0, 0, 0);
-    }
-  }
-  return acc;
-}
-
-// parameter p (state_dict order of one layer) -> (G row i, H column j) of its
-// gradient in the (layer, net) tile, or -1 when the gradient is zero by the mask
-// (the transformed-half inputs of the first Linear, the conditioning-half
-// outputs of the last).  Returns the net index through *net.
-template <int D, int H1, int H2, int NETS>
-__device__ __forceinline__ int param_cell(int r, int* net) {
-  using S = SP<D, H1, H2>;
-  constexpr int DT = S::DT, DC = S::DC, NL = S::NL;
-  constexpr int U[4] = {D, H1 ? H1 : D, H2 ? H2 : D, D};
-  constexpr int NFN = H1 == 0 ? D * D + D : (H2 == 0 ? H1 * D + H1 + D * H1 + D
-                                                      : H1 * D + H1 + H2 * H1 + H2 + D * H2 + D);
-  constexpr int HS = DC + H1 + H2 + 1;
-  *net = r / NFN;
-  r -= *net * NFN;
-  int gofs = 0, hofs = 0;
-#pragma unroll
-  for (int i = 0; i < NL; ++i) {
-    const int nin = U[i], nout = i == NL - 1 ? D : U[i + 1];
-    const bool first = i == 0, last = i == NL - 1;
-    const int nout_eff = last ? DT : nout, nin_eff = first ? DC : nin;
-    if (r < nout * nin) {
-      const int o = r / nin, col = r - o * nin;
-      const int kk = first ? col - DT : col;
-      return (o < nout_eff && kk >= 0 && kk < nin_eff) ? (gofs + o) * 16 + hofs + kk : -1;
-    }
-    r -= nout * nin;
-    if (r < nout) return r < nout_eff ? (gofs + r) * 16 + HS - 1 : -1;
-    r -= nout;
-    gofs += nout_eff;
-    hofs += nin_eff;
-  }
-  return -1;
-}
-
-// accumulator cell (G row i, H column j) -> offset of its parameter in the
-// net's state_dict block, or -1 (a cell of the dense tile with no parameter)
-template <int D, int H1, int H2>
-__device__ __forceinline__ int cell_param(int i, int j) {
-  using S = SP<D, H1, H2>;
-  constexpr int DT = S::DT, DC = S::DC, NL = S::NL;
-  constexpr int U[4] = {D, H1 ? H1 : D, H2 ? H2 : D, D};
-  constexpr int HS = DC + H1 + H2 + 1;
-  int gofs = 0, hofs = 0, woff = 0;
-#pragma unroll
-  for (int k = 0; k < NL; ++k) {
-    const int nin = U[k], nout = k == NL - 1 ? D : U[k + 1];
-    const bool first = k == 0, last = k == NL - 1;
-    const int nout_eff = last ? DT : nout, nin_eff = first ? DC : nin, in_off = first ? DT : 0;
-    if (i >= gofs && i < gofs + nout_eff) {
-      const int o = i - gofs;
-      if (j == HS - 1) return woff + nout * nin + o;
-      if (j >= hofs && j < hofs + nin_eff) return woff + o * nin + in_off + (j - hofs);
-      return -1;
-    }
-    woff += nout * nin + nout;
-    gofs += nout_eff;
-    hofs += nin_eff;
-  }
-  return -1;
-}
-
-template <int D, int H1, int H2, int NETS, bool LOSS, bool PERM>
-__global__ __launch_bounds__(64, 2) void k_vjp2(const float* __restrict__ W,
-                                                const int32_t* __restrict__ fq,
-                                                const int32_t* __restrict__ iq,
-                                                const int32_t* __restrict__ lflag, VArgs2 a) {
-  using S = SP<D, H1, H2>;
-  constexpr int DT = S::DT, DC = S::DC, NC = S::NC;
-  constexpr int LF = NETS * S::NF;
-  constexpr int GS = H1 + H2 + DT, HS = DC + H1 + H2 + 1;
-  static_assert(GS <= 16 && HS <= 16, "gradient stacks must fit one 16x16 MFMA tile");
-  constexpr int TF = kV2TR * D;
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* tile = smem;        // [TF] input rows
-  float* st = smem + TF;     // [32][kV2SS] G / H stage
-  const int lane = threadIdx.x;
-  const int64_t B = a.B;
-  const int L = a.L;
-  const int ntiles = (int)((B + kV2TR - 1) / kV2TR);
-  const f2 zero = splat(0.f, f2{});
-  constexpr float kLN2 = 0.69314718055994531f, kL2E = 1.4426950408889634f;
-  floatx4 acc[kV2LMax][NETS];
-#pragma unroll
-  for (int l = 0; l < kV2LMax; ++l)
-#pragma unroll
-    for (int n = 0; n < NETS; ++n) acc[l][n] = floatx4{0.f, 0.f, 0.f, 0.f};
-  for (int i = lane; i < 32 * kV2SS; i += 64) st[i] = 0.f;
-  float lt0 = 0.f, lt1 = 0.f, lt2 = 0.f;
-
-  for (int tix = blockIdx.x; tix < ntiles; tix += gridDim.x) {
-    const int64_t row0 = (int64_t)tix * kV2TR;
-    const int64_t r = row0 + 2 * lane;
-    const int nr = r >= B ? 0 : (r + 1 >= B ? 1 : 2);
-    // ---- rows in: one tile through LDS (full tiles: 16-B loads) ----
-    f2 v[D];
-    if (row0 + kV2TR <= B) {
-      wave_sync();
-      const float4* s4 = reinterpret_cast<const float4*>(a.x + row0 * D);
-      float4* d4 = reinterpret_cast<float4*>(tile);
-      for (int i = lane; i < TF / 4; i += 64) d4[i] = s4[i];
-      wave_sync();
-      f2 vv[1][D];
-      read_pairs<D, 1>(tile, lane, vv);
-#pragma unroll
-      for (int k = 0; k < D; ++k) v[k] = vv[0][k];
-    } else {
-#pragma unroll
-      for (int k = 0; k < D; ++k)
-        v[k] = f2{nr > 0 ? a.x[r * D + k] : 0.f, nr > 1 ? a.x[(r + 1) * D + k] : 0.f};
-    }
-    uint32_t lab = 0;
-    if constexpr (LOSS) lab = load_labels<D, 1>(a.y + r, nr, false);
-
-    // ---- forward sweep (plain weights, nothing stashed) ----
-    f2 ld = zero;
-    auto fwd = [&](auto O_, int l) __attribute__((always_inline)) {
-      constexpr bool O = decltype(O_)::value;
-      const float* wl = W + (int64_t)l * LF;
-      f2 c[DC];
-#pragma unroll
-      for (int k = 0; k < DC; ++k) c[k] = v[R<D, O>(DT + k)];
-      f2 h1[H1 ? H1 : 1], h2[H2 ? H2 : 1], t[DT], sv[DT];
-      {  // x_T of this layer, rows r, r+1: 2*DT contiguous floats
-        float* sp = a.stash + ((int64_t)l * B + r) * DT;
-#pragma unroll
-        for (int j = 0; j < DT; ++j) {
-          if (nr > 0) sp[j] = v[R<D, O>(j)].x;
-          if (nr > 1) sp[DT + j] = v[R<D, O>(j)].y;
-        }
-      }
-      vnet_fwd<S, NC>(wl + (NETS == 2 ? S::NF : 0), c, h1, h2, t);
-      if constexpr (NETS == 2) vnet_fwd<S, NC>(wl, c, h1, h2, sv);
-#pragma unroll
-      for (int j = 0; j < DT; ++j) {
-        f2& x = v[R<D, O>(j)];
-        if constexpr (NETS == 2) {
-          x = fmaV(x, exp2T(sv[j] * splat(kL2E, f2{})), t[j]);
-          ld += sv[j];
-        } else {
-          x += t[j];
-        }
-      }
-      if constexpr (PERM) {
-        if (lflag[l] & kFlagPerm) permute<D, O>(v, fq + l * D);
-      }
-    };
-    int l = 0;
-    for (; l + 1 < L; l += 2) {
-      fwd(std::false_type{}, l);
-      fwd(std::true_type{}, l + 1);
-    }
-    const bool oddL = l < L;
-    if (oddL) fwd(std::false_type{}, l);
-
-    // ---- upstream gradient at z_L (orientation L & 1) ----
-    f2 g[D];
-    f2 gld = zero;
-    auto seed = [&](auto O_) __attribute__((always_inline)) {
-      constexpr bool O = decltype(O_)::value;
-      if constexpr (LOSS) {
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          float z[D];
-#pragma unroll
-          for (int j = 0; j < D; ++j) z[j] = v[R<D, O>(j)][q];
-          float m = z[0];
-#pragma unroll
-          for (int j = 1; j < D; ++j) m = fmaxf(m, z[j]);
-          float se = 0.f;
-#pragma unroll
-          for (int j = 0; j < D; ++j) se += __builtin_amdgcn_exp2f((z[j] - m) * kL2E);
-          const float lse = m + __builtin_amdgcn_logf(se) * kLN2;
-          const uint32_t b = (lab >> (8 * q)) & 0xffu;
-          const bool ok = b != 0xffu, valid = q < nr;
-          const int yy = ok ? (int)b : 0;
-          uint32_t zb[D];
-#pragma unroll
-          for (int j = 0; j < D; ++j) zb[j] = __float_as_uint(z[j]);
-          const float lpy = __uint_as_float(sel_tree<D>(zb, yy, 0)) - lse;
-          const float ldq = NETS == 2 ? ld[q] : 0.f;  // plain weights: ld = sum(s)
-          float coef, ce_term, loss_row, gl;
-          if (a.kind == CNF_LOSS_CAL) {  // -(log(softmax(z)[y] + 1e-7) + ld)
-            const float py = __builtin_amdgcn_exp2f(lpy * kL2E);
-            ce_term = -__builtin_amdgcn_logf(py + kEps) * kLN2;
-            loss_row = ce_term - ldq;
-            coef = py / (py + kEps);
-            gl = -a.grad_scale;
-          } else {                       // CE(z, y) - det * ld
-            ce_term = -lpy;
-            loss_row = ce_term - a.det * ldq;
-            coef = 1.f;
-            gl = -a.det * a.grad_scale;
-          }
-          if (!ok) ce_term = loss_row = coef = __builtin_nanf("");
-          if (!valid) coef = gl = 0.f;
-#pragma unroll
-          for (int j = 0; j < D; ++j) {
-            const float pj = __builtin_amdgcn_exp2f((z[j] - lse) * kL2E);
-            g[R<D, O>(j)][q] = a.grad_scale * coef * (pj - (j == yy ? 1.f : 0.f));
-          }
-          gld[q] = gl;
-          if (valid) {
-            lt0 += loss_row;
-            lt1 += ce_term;
-            lt2 += ldq;
-          }
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < D; ++j)
-          g[R<D, O>(j)] = f2{a.gz && nr > 0 ? a.gz[r * D + j] : 0.f,
-                              a.gz && nr > 1 ? a.gz[(r + 1) * D + j] : 0.f};
-        gld = f2{a.gld && nr > 0 ? a.gld[r] : 0.f, a.gld && nr > 1 ? a.gld[r + 1] : 0.f};
-      }
-    };
-    if (oddL) seed(std::true_type{});
-    else seed(std::false_type{});
-
-    // ---- backward sweep ----
-    // layer index compile-time (static_for below): the per-layer gradient
-    // accumulators acc[l][net] stay in registers (a runtime-indexed select
-    // over them was lowered to scratch)
-    auto bwd = [&](auto LI) __attribute__((always_inline)) {
-      constexpr int l = decltype(LI)::value;
-      constexpr bool Oc = ((l + 1) & 1) != 0;  // orientation of z_l
-      constexpr bool Oi = !Oc;
-      if (a.gz_all) {
-#pragma unroll
-        for (int j = 0; j < D; ++j)
-          g[R<D, Oc>(j)] += f2{nr > 0 ? a.gz_all[((int64_t)l * B + r) * D + j] : 0.f,
-                               nr > 1 ? a.gz_all[((int64_t)l * B + r + 1) * D + j] : 0.f};
-      }
-      if constexpr (PERM) {
-        if (lflag[l] & kFlagPerm) {  // undo z[:, perm].flip(1): z_pre[i] = z_out[iq[i]]
-          permute<D, Oc>(v, iq + l * D);
-          permute<D, Oc>(g, iq + l * D);
-        }
-      }
-      const float* wl = W + (int64_t)l * LF;
-      f2 c[DC], gT[DT], gc[DC];
-#pragma unroll
-      for (int k = 0; k < DC; ++k) {
-        c[k] = v[R<D, Oi>(DT + k)];
-        gc[k] = zero;
-      }
-#pragma unroll
-      for (int j = 0; j < DT; ++j) gT[j] = g[R<D, Oi>(j)];
-      f2 xT[DT];
-      {
-        const float* sp = a.stash + ((int64_t)l * B + r) * DT;
-#pragma unroll
-        for (int j = 0; j < DT; ++j) xT[j] = f2{nr > 0 ? sp[j] : 0.f, nr > 1 ? sp[DT + j] : 0.f};
-      }
-      f2 th1[H1 ? H1 : 1], th2[H2 ? H2 : 1], t[DT];
-      vnet_fwd<S, NC>(wl + (NETS == 2 ? S::NF : 0), c, th1, th2, t);
-      f2 H[HS];
-#pragma unroll
-      for (int k = 0; k < DC; ++k) H[k] = c[k];
-      H[HS - 1] = splat(1.f, f2{});
-      // invalid (padding) rows contribute nothing to the weight gradients
-      const f2 keep = f2{nr > 0 ? 1.f : 0.f, nr > 1 ? 1.f : 0.f};
-      if constexpr (NETS == 2) {
-        f2 sh1[H1 ? H1 : 1], sh2[H2 ? H2 : 1], sv[DT];
-        vnet_fwd<S, NC>(wl, c, sh1, sh2, sv);
-        f2 gs[DT];
-#pragma unroll
-        for (int j = 0; j < DT; ++j) {
-          const f2 e = exp2T(sv[j] * splat(kL2E, f2{}));
-          gs[j] = fmaV(gT[j] * xT[j], e, gld);  // z_T = x_T e^s + t, ld += s
-          gT[j] = gT[j] * e;
-        }
-        f2 G[GS];
-        vnet_bwd<S, NC>(wl, sh1, sh2, gs, gc, G);
-#pragma unroll
-        for (int f = 0; f < GS; ++f) G[f] *= keep;
-#pragma unroll
-        for (int m = 0; m < H1; ++m) H[DC + m] = sh1[m];
-#pragma unroll
-        for (int m = 0; m < H2; ++m) H[DC + H1 + m] = sh2[m];
-        acc[l][0] = wgrad_tile<GS, HS>(st, G, H, lane, acc[l][0]);
-      }
-      {  // t-net: d/dt = g_T (before the e^s scaling of the s-net branch)
-        f2 G[GS];
-        f2 gt[DT];
-#pragma unroll
-        for (int j = 0; j < DT; ++j) gt[j] = g[R<D, Oi>(j)];
-        vnet_bwd<S, NC>(wl + (NETS == 2 ? S::NF : 0), th1, th2, gt, gc, G);
-#pragma unroll
-        for (int f = 0; f < GS; ++f) G[f] *= keep;
-#pragma unroll
-        for (int m = 0; m < H1; ++m) H[DC + m] = th1[m];
-#pragma unroll
-        for (int m = 0; m < H2; ++m) H[DC + H1 + m] = th2[m];
-        acc[l][NETS - 1] = wgrad_tile<GS, HS>(st, G, H, lane, acc[l][NETS - 1]);
-      }
-#pragma unroll
-      for (int j = 0; j < DT; ++j) {
-        v[R<D, Oi>(j)] = xT[j];
-        g[R<D, Oi>(j)] = gT[j];
-      }
-#pragma unroll
-      for (int k = 0; k < DC; ++k) g[R<D, Oi>(DT + k)] += gc[k];
-    };
-    static_for<0, kV2LMax>([&](auto I) __attribute__((always_inline)) {
-      constexpr int l = kV2LMax - 1 - decltype(I)::value;
-      if (l < L) bwd(std::integral_constant<int, l>{});
-    });
-    if (a.dx) {
-#pragma unroll
-      for (int j = 0; j < D; ++j) {
-        if (nr > 0) a.dx[r * D + j] = g[j].x;
-        if (nr > 1) a.dx[(r + 1) * D + j] = g[j].y;
-      }
-    }
-  }
-
-  // ---- this wave's partial: parameter gradients (state_dict order) + loss sums ----
-  float* out = a.partials + (int64_t)blockIdx.x * a.PS;
-  const int P = a.P;
-  constexpr int NFN = H1 == 0 ? D * D + D : (H2 == 0 ? H1 * D + H1 + D * H1 + D
-                                                      : H1 * D + H1 + H2 * H1 + H2 + D * H2 + D);
-  // zeros where the mask makes the gradient vanish
-  for (int p = lane; p < P; p += 64) {
-    int n;
-    const int l = p / (NETS * NFN);
-    if (param_cell<D, H1, H2, NETS>(p - l * NETS * NFN, &n) < 0) out[p] = 0.f;
-  }
-  // the lane's accumulator cells: C[i = 4 (lane/16) + e][j = lane % 16]
-  const int j = lane & 15, i0 = 4 * (lane >> 4);
-  static_for<0, kV2LMax>([&](auto I) __attribute__((always_inline)) {
-    constexpr int l = decltype(I)::value;
-    if (l >= L) return;
-#pragma unroll
-    for (int n = 0; n < NETS; ++n) {
-      const floatx4 c4 = acc[l][n];
-      // net n's parameters follow the layer's state_dict order: s-net first
-      const int base = l * NETS * NFN + n * NFN;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int q = cell_param<D, H1, H2>(i0 + e, j);
-        if (q >= 0) out[base + q] = c4[e];
-      }
-    }
-  });
-  if constexpr (LOSS) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-      lt0 += __shfl_xor(lt0, off);
-      lt1 += __shfl_xor(lt1, off);
-      lt2 += __shfl_xor(lt2, off);
-    }
-    if (lane == 0) {
-      out[P] = lt0;
-      out[P + 1] = lt1;
-      out[P + 2] = lt2;
-    }
-  }
-}
-
 using VFn = void (*)(const float*, const int32_t*, const int32_t*, const int32_t*, const float*,
                      const int64_t*, const float*, const float*, const float*, float*, float*,
                      int64_t, int, int, int, int, int, float, float, int, int);
@@ -1152,37 +594,21 @@ int64_t grid_for(int64_t B) {
 
 int partial_stride(const Shape& s) { return (int)(((s.layer_floats * s.L + 3) + 3) & ~3); }
 
-using VFn2 = void (*)(const float*, const int32_t*, const int32_t*, const int32_t*, VArgs2);
-
-struct V2Entry {
-  int D, H1, H2;
-  VFn2 fn[2][2][2];  // [nets - 1][loss][perm]
-};
-
-#define CNF_V2N(D, H1, H2, N)                                                        \
-  {{k_vjp2<D, H1, H2, N, false, false>, k_vjp2<D, H1, H2, N, false, true>},          \
-   {k_vjp2<D, H1, H2, N, true, false>, k_vjp2<D, H1, H2, N, true, true>}}
-#define CNF_V2(D, H1, H2) {D, H1, H2, {CNF_V2N(D, H1, H2, 1), CNF_V2N(D, H1, H2, 2)}}
-
-// the packed-SGPR shapes (cnf_sgpr.hip's table): every one has GS, HS <= 16
-const V2Entry kV2Table[] = {
-#ifdef CNF_VJP_DEV
-    CNF_V2(10, 5, 5),
-#else
-    CNF_V2(2, 5, 5), CNF_V2(3, 5, 5), CNF_V2(4, 5, 5), CNF_V2(5, 5, 5),
-    CNF_V2(6, 5, 5), CNF_V2(8, 5, 5), CNF_V2(10, 5, 5),
-    CNF_V2(3, 3, 3), CNF_V2(8, 3, 3), CNF_V2(10, 3, 3),
-    CNF_V2(3, 3, 0), CNF_V2(3, 0, 0), CNF_V2(10, 0, 0),
-    CNF_V2(10, 5, 0), CNF_V2(3, 5, 0),
-#endif
-};
+using v2::kV2TR;
+using v2::kV2LMax;
+using v2::kV2SS;
 
 const V2Entry* find_v2(const Shape& s) {
   if (s.family != Family::kValu || s.strict || !s.sp_ok || !s.shift || s.L > kV2LMax)
     return nullptr;
   const int h1 = s.n_lin >= 2 ? s.units[1] : 0, h2 = s.n_lin >= 3 ? s.units[2] : 0;
-  for (const auto& e : kV2Table)
-    if (e.D == s.D && e.H1 == h1 && e.H2 == h2) return &e;
+  const V2Entry* parts[3] = {kV2PartA, kV2PartB, kV2PartC};
+  const int nums[3] = {kV2PartANum, kV2PartBNum, kV2PartCNum};
+  for (int q = 0; q < 3; ++q)
+    for (int i = 0; i < nums[q]; ++i) {
+      const V2Entry& e = parts[q][i];
+      if (e.D == s.D && e.H1 == h1 && e.H2 == h2) return &e;
+    }
   return nullptr;
 }
 
