@@ -23,6 +23,32 @@ calibrator losses apply.
 Native path: the stack runs as cnf_desc options CNF_OPT_ALT_MASK (| S_TANH) on
 the flip-based kernels with odd layers' weights reversed at prepare time
 (include/cnf.h); gradients come back in this module's parameter layout.
+
+The Keras-era NICE flows of code-old/nice.py are restated here too
+(`LegacyNiceFlow`, version=1/2/3), additive (log-det 0, as the Keras models
+have none):
+
+* version 1, `NiceFlow` (code-old/nice.py:101-145) with the split coupling
+  `AddCouplingLayer` (:55-77): x1 = x[:, :D//2], x2 = x[:, D//2:]; layer l
+  even ('odd' mode): x2 += f_l(x1), f_l: D//2 -> D-D//2; layer l odd ('even'
+  mode): x1 += f_l(x2), f_l: D-D//2 -> D//2.  No permutation.
+* version 2, `NiceFlow_v2` (:158-211): every layer 'even' mode (x1 += f(x2))
+  followed by a full reversal (`ReIndex`), one more reversal at the end for
+  odd L.
+* version 3, `NiceFlow_v3` (:214-263) with `AddCouplingLayer_v2` (:80-98):
+  y = b*x + (1-b)*(x + f(b*x)), f = MLP(D -> D), the mask b = [0]*(D//2) +
+  [1]*(D-D//2) flipped every layer; no data permutation.
+
+`backward` is the true inverse for every version.  (The Keras v3 inverse
+model, code-old/nice.py:232-245, applies the coupling functions in FORWARD
+order with the reversed mask sequence -- it inverts only when every f_l is the
+same function; that quirk is not reproduced.)
+
+Versions 1 and 2 keep Keras' half-width conditioners (the torch restatement is
+their only implementation; on a ROCm device they run torch ops, reported
+through flows.flows._not_native).  Version 3 is the alternate-mask stack of the
+RealNVP path with the s-net absent, so it runs natively as CNF_OPT_ALT_MASK on
+the shift-only kernels.
 """
 import torch
 import torch.nn.functional as F
@@ -139,4 +165,180 @@ class LegacyRealNvpFlow(nn.Module):
         for ly in reversed(self.layers):
             y, l = ly.backward(y)
             ld = ld + l
+        return y, ld
+
+
+def _mlp(n_in, hidden, n_out, act):
+    """Keras MLP(input_dim, output_dim, hidden_size, activation)
+    (code-old/nice.py:8-16): Dense(h, act) ... Dense(output_dim)."""
+    widths = [n_in, *hidden, n_out]
+    lins = nn.ModuleList(nn.Linear(a, b) for a, b in zip(widths[:-1], widths[1:]))
+    return lins
+
+
+def _run_mlp(lins, act, x):
+    *hidden, last = lins
+    for lin in hidden:
+        x = act(lin(x))
+    return last(x)
+
+
+class LegacySplitCoupling(nn.Module):
+    """AddCouplingLayer (code-old/nice.py:55-77): split x into x1 (first D//2)
+    and x2 (rest); mode 'odd': x2 + f(x1); mode 'even': x1 + f(x2); inverse
+    subtracts."""
+
+    def __init__(self, dim, hidden_size, mode, activation="relu"):
+        super().__init__()
+        self.dim = dim
+        self.mode = mode
+        self.activation = activation
+        h = dim // 2
+        n_in, n_out = (h, dim - h) if mode == "odd" else (dim - h, h)
+        self.f = _mlp(n_in, list(hidden_size), n_out, _ACT[activation])
+
+    def _couple(self, x, sign):
+        h = self.dim // 2
+        x1, x2 = x[:, :h], x[:, h:]
+        if self.mode == "odd":
+            x2 = x2 + sign * _run_mlp(self.f, _ACT[self.activation], x1)
+        else:
+            x1 = x1 + sign * _run_mlp(self.f, _ACT[self.activation], x2)
+        return torch.cat([x1, x2], dim=1)
+
+    def forward(self, x):
+        return self._couple(x, 1.0)
+
+    def backward(self, y):
+        return self._couple(y, -1.0)
+
+
+class LegacyAddCoupling(nn.Module):
+    """AddCouplingLayer_v2 (code-old/nice.py:80-98): y = b*x + (1-b)*(x +
+    f(b*x)), f = MLP(dim -> dim); inverse: (1-b)*(y - f(b*y)).  The mask
+    parity follows NiceFlow_v3 (:214-230): [0]*(D//2)+[1]*(D-D//2), flipped on
+    odd layers.  Attributes the native stack reads: scale False (no s-net),
+    shift True, t = the conditioner."""
+
+    def __init__(self, dim, hidden_size, parity, activation="relu"):
+        super().__init__()
+        self.dim = dim
+        self.hidden_size = list(hidden_size)
+        self.parity = int(parity) & 1
+        self.activation = activation
+        self.s_activation = activation
+        self.s = None
+        self.t = MLP(dim, self.hidden_size, _ACT[activation])
+        b = torch.zeros(1, dim)
+        b[:, dim // 2:] = 1.0
+        if self.parity:
+            b = b.flip(1)
+        self.register_buffer("mask", b)
+        self.scale = False
+        self.shift = True
+        self.random_flip = False
+        self.invertible = True
+
+    def forward(self, x):
+        b = self.mask
+        x_b = b * x
+        y = x_b + (1 - b) * (x + self.t(x_b))
+        return y, torch.zeros(x.shape[0], dtype=x.dtype, device=x.device)
+
+    def backward(self, y):
+        b = self.mask
+        y_b = b * y
+        x = y_b + (1 - b) * (y - self.t(y_b))
+        return x, torch.zeros(y.shape[0], dtype=y.dtype, device=y.device)
+
+
+class LegacyNiceFlow(nn.Module):
+    """The NICE flows of code-old/nice.py in torch (see the module docstring):
+    version 1 `NiceFlow`, 2 `NiceFlow_v2`, 3 `NiceFlow_v3`; default hidden
+    [dim], 4 layers (:104-111).  forward(x) -> (y, ld = 0); backward(y) ->
+    (x, ld = 0)."""
+
+    def __init__(self, dim, layers=4, hidden_size=None, activation="relu", version=1, **kwargs):
+        super().__init__()
+        hidden_size = [dim] if hidden_size is None else list(hidden_size)
+        if version not in (1, 2, 3):
+            raise ValueError("LegacyNiceFlow version must be 1, 2 or 3")
+        self.dim = dim
+        self.version = version
+        self.n_layers = layers
+        if version == 1:
+            mods = [LegacySplitCoupling(dim, hidden_size, "even" if l % 2 else "odd", activation)
+                    for l in range(layers)]
+        elif version == 2:
+            mods = [LegacySplitCoupling(dim, hidden_size, "even", activation) for _ in range(layers)]
+        else:
+            mods = [LegacyAddCoupling(dim, hidden_size, l, activation) for l in range(layers)]
+        self.layers = nn.ModuleList(mods)
+        self.invertible = True
+        self._stack = None
+
+    # -- native plumbing (version 3) ---------------------------------------
+    def _native_ok(self, x):
+        if not (isinstance(x, torch.Tensor) and x.is_cuda and x.dtype == torch.float32
+                and x.dim() == 2 and x.shape[1] == self.dim):
+            return False
+        from flows.flows import _not_native
+        if self.version != 3:
+            _not_native("legacy NiceFlow version %d (half-width split conditioners)"
+                        % self.version)
+            return False
+        if self.layers[0].activation != "relu":
+            _not_native("legacy NICE activation %r" % self.layers[0].activation)
+            return False
+        return True
+
+    def _native_stack(self):
+        if self._stack is None:
+            from cnf_hip import _lib
+            from cnf_hip.engine import CouplingStack
+            self._stack = CouplingStack(list(self.layers), options=_lib.OPT_ALT_MASK)
+        return self._stack
+
+    def invalidate_native(self):
+        self._stack = None
+
+    def __getstate__(self):
+        st = self.__dict__.copy()
+        st["_stack"] = None
+        return st
+
+    @staticmethod
+    def _rev(x):
+        return x.flip(1)  # ReIndex() with the default index (code-old/nice.py:38-51)
+
+    def forward(self, x):
+        if self._native_ok(x):
+            stack = self._native_stack()
+            if torch.is_grad_enabled() and (x.requires_grad or stack.requires_grad()):
+                return stack.forward_autograd(x, want_all=False)
+            y, ld, _ = stack.run(x)
+            return y, ld
+        ld = torch.zeros(x.shape[0], dtype=x.dtype, device=x.device)
+        for ly in self.layers:
+            x = ly(x)[0] if self.version == 3 else ly(x)
+            if self.version == 2:
+                x = self._rev(x)
+        if self.version == 2 and len(self.layers) % 2 == 1:
+            x = self._rev(x)
+        return x, ld
+
+    def backward(self, y):
+        if self._native_ok(y):
+            stack = self._native_stack()
+            if torch.is_grad_enabled() and (y.requires_grad or stack.requires_grad()):
+                return stack.inverse_autograd(y, want_all=False)
+            x, ld, _ = stack.run(y, inverse=True)
+            return x, ld
+        ld = torch.zeros(y.shape[0], dtype=y.dtype, device=y.device)
+        if self.version == 2 and len(self.layers) % 2 == 1:
+            y = self._rev(y)
+        for ly in reversed(self.layers):
+            if self.version == 2:
+                y = self._rev(y)
+            y = ly.backward(y)[0] if self.version == 3 else ly.backward(y)
         return y, ld

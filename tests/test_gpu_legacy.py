@@ -70,3 +70,69 @@ def test_legacy_forward_inverse_and_grads(D, L, hidden, s_act):
         assert (p.grad.cpu() - g_ref[k]).abs().max().item() / sc <= 1e-4, k
     sc = gx_ref.abs().max().item() + 1e-3
     assert (xg.grad.cpu() - gx_ref).abs().max().item() / sc <= 1e-4
+
+
+@pytest.mark.parametrize("D,L,hidden", [
+    (10, 4, [10]),      # code-old/nice.py defaults: hidden [dim], layers 4
+    (7, 3, [5, 5]),     # odd D, odd L
+    (100, 2, [100]),
+])
+def test_legacy_nice_v3_native_matches_restatement(D, L, hidden):
+    """NiceFlow_v3 (code-old/nice.py:214-263) as CNF_OPT_ALT_MASK on the
+    shift-only kernels: forward, inverse and gradients vs the CPU torch
+    restatement (parity unpinned: TensorFlow absent)."""
+    from flows.legacy import LegacyNiceFlow
+    torch.manual_seed(0)
+    f = LegacyNiceFlow(D, layers=L, hidden_size=hidden, version=3)
+    g = torch.Generator().manual_seed(1)
+    with torch.no_grad():
+        for p in f.parameters():
+            p.copy_(torch.randn(p.shape, generator=g) * (0.2 if D <= 20 else 0.05))
+    x = torch.randn(257, D, generator=torch.Generator().manual_seed(3))
+    w = torch.randn(257, D, generator=torch.Generator().manual_seed(4))
+    with torch.no_grad():
+        y_ref, _ = f(x)
+        x_back, _ = f.backward(y_ref)
+    xc = x.clone().requires_grad_(True)
+    (f(xc)[0] * w).sum().backward()
+    g_ref = {k: p.grad.clone() for k, p in f.named_parameters()}
+    gx_ref = xc.grad.clone()
+
+    fg = f.to(DEV)
+    assert fg._native_stack().kernel_name() == "mfma-tile"
+    n0 = engine.stats["forward"] + engine.stats["inverse"]
+    with torch.no_grad():
+        y, ld = fg(x.to(DEV))
+        xb, ild = fg.backward(y_ref.to(DEV))
+    assert engine.stats["forward"] + engine.stats["inverse"] >= n0 + 2, "native path did not run"
+    assert _rel(y.cpu(), y_ref) <= 1e-5 and _rel(xb.cpu(), x_back) <= 1e-5
+    assert ld.abs().max().item() == 0 and ild.abs().max().item() == 0
+    fg.zero_grad()
+    xg = x.to(DEV).requires_grad_(True)
+    (fg(xg)[0] * w.to(DEV)).sum().backward()
+    for k, p in fg.named_parameters():
+        sc = g_ref[k].abs().max().item() + 1e-3
+        assert (p.grad.cpu() - g_ref[k]).abs().max().item() / sc <= 1e-4, k
+    sc = gx_ref.abs().max().item() + 1e-3
+    assert (xg.grad.cpu() - gx_ref).abs().max().item() / sc <= 1e-4
+
+
+def test_legacy_nice_split_versions_report_torch_execution():
+    """NiceFlow / NiceFlow_v2 keep Keras' half-width conditioners: on the GPU
+    they run torch ops and say so (RuntimeWarning, or an error under
+    CNF_STRICT_NATIVE), with results equal to the CPU restatement."""
+    from flows.legacy import LegacyNiceFlow
+    for version in (1, 2):
+        torch.manual_seed(0)
+        f = LegacyNiceFlow(10, layers=3, version=version)
+        x = torch.randn(64, 10)
+        with torch.no_grad():
+            y_ref, _ = f(x)
+        fg = f.to(DEV)
+        with pytest.warns(RuntimeWarning, match="legacy NiceFlow version"):
+            import flows.flows as FF
+            FF._warned.discard("legacy NiceFlow version %d (half-width split conditioners)"
+                               % version)
+            with torch.no_grad():
+                y, _ = fg(x.to(DEV))
+        assert _rel(y.cpu(), y_ref) <= 1e-5

@@ -81,3 +81,109 @@ def test_factory_options_select_the_legacy_flow():
     assert z.shape == (5, 6)
     with pytest.raises(ValueError):
         RealNvpFlow(6, mask_mode="bogus")
+
+
+# ---- legacy NICE (code-old/nice.py; flows/legacy.py LegacyNiceFlow) ----
+
+def _nice(D, L, hidden, version, seed=0, sigma=0.3):
+    from flows.legacy import LegacyNiceFlow
+    torch.manual_seed(seed)
+    f = LegacyNiceFlow(D, layers=L, hidden_size=hidden, version=version)
+    g = torch.Generator().manual_seed(seed + 1)
+    with torch.no_grad():
+        for p in f.parameters():
+            p.copy_(torch.randn(p.shape, generator=g) * sigma)
+    return f
+
+
+@pytest.mark.parametrize("version", [1, 2, 3])
+@pytest.mark.parametrize("D,L", [(10, 4), (7, 3), (3, 2), (6, 1)])
+def test_legacy_nice_round_trips_with_zero_logdet(version, D, L):
+    f = _nice(D, L, [D], version)
+    x = torch.randn(64, D, generator=torch.Generator().manual_seed(2))
+    with torch.no_grad():
+        y, ld = f(x)
+        xb, ild = f.backward(y)
+    assert torch.allclose(xb, x, atol=1e-5)
+    assert not torch.allclose(y, x, atol=1e-3)
+    assert torch.count_nonzero(ld) == 0 and torch.count_nonzero(ild) == 0
+
+
+def test_legacy_nice_v1_split_coupling_by_hand():
+    """NiceFlow (code-old/nice.py:101-145): layer 0 ('odd') x2 += f0(x1),
+    layer 1 ('even') x1 += f1(x2), no permutation."""
+    D = 7
+    f = _nice(D, 2, [5], 1)
+    x = torch.randn(16, D, generator=torch.Generator().manual_seed(5))
+    relu = torch.relu
+
+    def mlp(lins, v):
+        return lins[1](relu(lins[0](v)))
+    with torch.no_grad():
+        x1, x2 = x[:, :3], x[:, 3:]
+        x2 = x2 + mlp(f.layers[0].f, x1)
+        x1 = x1 + mlp(f.layers[1].f, x2)
+        want = torch.cat([x1, x2], 1)
+        got, _ = f(x)
+    assert f.layers[0].f[0].in_features == 3 and f.layers[0].f[-1].out_features == 4
+    assert f.layers[1].f[0].in_features == 4 and f.layers[1].f[-1].out_features == 3
+    assert torch.allclose(got, want, atol=1e-6)
+
+
+@pytest.mark.parametrize("D,L", [(10, 4), (7, 3)])
+def test_legacy_nice_v2_equals_maintained_nice_flow(D, L):
+    """NiceFlow_v2 (x1 += f(x2), then a full reversal per layer, one more for
+    odd L) is the maintained NICE flow (flows/flows.py, scale=False) with the
+    half-width conditioner embedded in the full-width t-net."""
+    f = _nice(D, L, [5], 2)
+    h = D // 2
+    layers = [NvpCouplingLayer(D, [5], scale=False) for _ in range(L)]
+    with torch.no_grad():
+        for ly, lf in zip(layers, f.layers):
+            l0, l1 = ly.t.layers
+            l0.weight.zero_()
+            l0.weight[:, h:] = lf.f[0].weight
+            l0.bias.copy_(lf.f[0].bias)
+            l1.weight.zero_()
+            l1.bias.zero_()
+            l1.weight[:h] = lf.f[1].weight
+            l1.bias[:h] = lf.f[1].bias
+        x = torch.randn(32, D, generator=torch.Generator().manual_seed(9))
+        zs, _ = Flow(layers)(x)
+        want = zs[-1].flip(1) if L % 2 else zs[-1]
+        got, _ = f(x)
+    assert torch.allclose(got, want, atol=1e-5)
+
+
+@pytest.mark.parametrize("D,L", [(10, 4), (7, 3)])
+def test_legacy_nice_v3_is_the_additive_alternate_mask_flow(D, L):
+    """NiceFlow_v3 (AddCouplingLayer_v2, flipped mask per layer) equals the
+    alternate-mask RealNVP restatement with the s-net identically zero."""
+    f = _nice(D, L, [D], 3)
+    r = _legacy(D, L, [D], "relu")
+    with torch.no_grad():
+        for lr, lf in zip(r.layers, f.layers):
+            for lin in lr.s.layers:
+                lin.weight.zero_()
+                lin.bias.zero_()
+            for a, b in zip(lr.t.layers, lf.t.layers):
+                a.weight.copy_(b.weight)
+                a.bias.copy_(b.bias)
+        x = torch.randn(32, D, generator=torch.Generator().manual_seed(11))
+        want, _ = r(x)
+        got, _ = f(x)
+    assert torch.allclose(got, want, atol=1e-6)
+
+
+def test_nice_factory_legacy_option():
+    from flows.legacy import LegacyNiceFlow
+    from flows.nice_torch import NiceFlow
+    for v in (1, 2, 3):
+        f = NiceFlow(6, layers=3, hidden_size=[4], legacy=v, dev="cpu", epochs=2)
+        assert isinstance(f, LegacyNiceFlow) and f.version == v and len(f.layers) == 3
+        y, ld = f(torch.randn(5, 6))
+        assert y.shape == (5, 6) and ld.shape == (5,)
+    g = NiceFlow(6, layers=2)
+    assert isinstance(g, NiceFlow) and not isinstance(g, LegacyNiceFlow)
+    with pytest.raises(ValueError):
+        NiceFlow(6, legacy=4)
