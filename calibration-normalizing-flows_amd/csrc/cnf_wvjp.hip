@@ -251,8 +251,11 @@ struct DwArgs {
   int64_t M, rows, PS;
 };
 
+#ifndef CNF_DW_WPS
+#define CNF_DW_WPS 1
+#endif
 template <int NC>
-__global__ __launch_bounds__(64) void k_wdw(DwArgs da) {
+__global__ __launch_bounds__(64, CNF_DW_WPS) void k_wdw(DwArgs da) {
   const DwJob& j = da.job[blockIdx.y];
   const int lane = threadIdx.x, i = lane & 31, h = lane >> 5;
   const int nsub = (j.N + 31) >> 5;
@@ -349,6 +352,17 @@ struct Geo {
   __device__ __forceinline__ int col(int i) const { return i < DT ? Cp + i : i - DT; }
 };
 
+// A layer's gather table (D <= CNF_MAX_DIM ints) staged in LDS once per block:
+// the row loops then index it without a dependent global load per element
+// (the table lookups had put two serialized memory round trips into every
+// row's update).
+__device__ __forceinline__ const int32_t* stage_table(int32_t* sq, const int32_t* __restrict__ q,
+                                                      int D) {
+  for (int j = threadIdx.x; j < D; j += blockDim.x) sq[j] = q[j];
+  __syncthreads();
+  return sq;
+}
+
 // Natural [B][D] rows -> stash layout (the first layer's input).
 __global__ __launch_bounds__(256) void k_wstash(const float* __restrict__ x,
                                                 float* __restrict__ xs, int64_t B, Geo g) {
@@ -369,34 +383,65 @@ __global__ __launch_bounds__(256) void k_wstash(const float* __restrict__ x,
 // Coupling update of one layer (flows/flows.py:101-112), one wave per row:
 //   z_i = x_i e^{s_i} + t_i (i < DT), x_i otherwise; ld += sum_i s_i;
 //   out[j] = z[fq[j]] (permutation, then flip); stash layout in and out.
+// A wave takes kRU rows at a time and issues every load of the group before
+// the first use (lane l: columns j = l + 64q), so a wave has kRU rows of
+// loads in flight instead of one row's dependent round trips.
+constexpr int kRU = 4;                   // rows per wave per group
+constexpr int kNJ = CNF_MAX_DIM / 64;    // column slots per lane
 __global__ __launch_bounds__(256) void k_wfwd_update(const float* __restrict__ X,
                                                      float* __restrict__ Xn, float* __restrict__ ld,
                                                      const float* __restrict__ Os,
                                                      const float* __restrict__ Ot,
-                                                     const int32_t* __restrict__ fq, int64_t B,
+                                                     const int32_t* __restrict__ fqg, int64_t B,
                                                      Geo g, int first) {
+  __shared__ int32_t sq[CNF_MAX_DIM];
+  const int32_t* fq = stage_table(sq, fqg, g.D);
   const int lane = threadIdx.x & 63;
+  int ii[kNJ];
+#pragma unroll
+  for (int q = 0; q < kNJ; ++q) ii[q] = lane + 64 * q < g.D ? fq[lane + 64 * q] : 0;
   const int64_t nw = (int64_t)gridDim.x * 4;
-  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < B; r += nw) {
-    const float* xr = X + r * g.Dp;
-    float* zr = Xn + r * g.Dp;
-    float sacc = 0.f;
-    for (int j = lane; j < g.D; j += 64) {
-      const int i = fq[j];
-      float v = xr[g.col(i)];
-      if (i < g.DT) {
-        const float s = Os ? Os[r * g.DTp + i] : 0.f;
-        const float t = Ot ? Ot[r * g.DTp + i] : 0.f;
-        v = __fadd_rn(__fmul_rn(v, expf(s)), t);
+  for (int64_t r0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * kRU; r0 < B; r0 += nw * kRU) {
+    float v[kRU][kNJ], sv[kRU][kNJ], tv[kRU][kNJ], so[kRU][kNJ], ldo[kRU];
+#pragma unroll
+    for (int u = 0; u < kRU; ++u) {
+      const int64_t r = r0 + u < B ? r0 + u : B - 1;  // past-the-end rows: loads only
+      ldo[u] = first ? 0.f : ld[r];
+#pragma unroll
+      for (int q = 0; q < kNJ; ++q) {
+        const int j = lane + 64 * q, i = ii[q];
+        v[u][q] = sv[u][q] = tv[u][q] = so[u][q] = 0.f;
+        if (j < g.D) {
+          v[u][q] = X[r * g.Dp + g.col(i)];
+          if (i < g.DT) {
+            if (Os) sv[u][q] = Os[r * g.DTp + i];
+            if (Ot) tv[u][q] = Ot[r * g.DTp + i];
+          }
+        }
+        if (Os && j < g.DT) so[u][q] = Os[r * g.DTp + j];
       }
-      zr[g.col(j)] = v;
     }
-    if (Os)
-      for (int i = lane; i < g.DT; i += 64) sacc += Os[r * g.DTp + i];
-    for (int c = g.DC + lane; c < g.Cp; c += 64) zr[c] = c == g.DC ? 1.f : 0.f;
-    for (int c = g.Cp + g.DT + lane; c < g.Dp; c += 64) zr[c] = 0.f;
-    sacc = wave_sum(sacc);
-    if (lane == 0) ld[r] = first ? sacc : ld[r] + sacc;
+#pragma unroll
+    for (int u = 0; u < kRU; ++u) {
+      const int64_t r = r0 + u;
+      if (r >= B) break;
+      float* zr = Xn + r * g.Dp;
+      float sacc = 0.f;
+#pragma unroll
+      for (int q = 0; q < kNJ; ++q) {
+        const int j = lane + 64 * q;
+        if (j < g.D) {
+          float x = v[u][q];
+          if (ii[q] < g.DT) x = __fadd_rn(__fmul_rn(x, expf(sv[u][q])), tv[u][q]);
+          zr[g.col(j)] = x;
+        }
+        sacc += so[u][q];
+      }
+      for (int c = g.DC + lane; c < g.Cp; c += 64) zr[c] = c == g.DC ? 1.f : 0.f;
+      for (int c = g.Cp + g.DT + lane; c < g.Dp; c += 64) zr[c] = 0.f;
+      sacc = wave_sum(sacc);
+      if (lane == 0) ld[r] = first ? sacc : ldo[u] + sacc;
+    }
   }
 }
 
@@ -485,32 +530,63 @@ __global__ __launch_bounds__(256) void k_wseed(const float* __restrict__ Z,
 //   G_s = g_pre_T x_T e + gld,  G_t = g_pre_T,  g_in_T = g_pre_T e,
 //   g_in_C = g_pre_C (the conditioners' share is added by the first Linear's
 //   back-prop), plus the caller's gradient of the previous layer's output.
+// kRU rows per wave with every load of the group issued first (as k_wfwd_update).
 __global__ __launch_bounds__(256) void k_wbwd_update(
     const float* __restrict__ gout, float* __restrict__ gin, const float* __restrict__ X,
     const float* __restrict__ Os, const float* __restrict__ gld, float* __restrict__ Gs,
-    float* __restrict__ Gt, const float* __restrict__ gprev, const int32_t* __restrict__ fq,
+    float* __restrict__ Gt, const float* __restrict__ gprev, const int32_t* __restrict__ fqg,
     int64_t B, Geo g) {
+  __shared__ int32_t sq[CNF_MAX_DIM];
+  const int32_t* fq = stage_table(sq, fqg, g.D);
   const int lane = threadIdx.x & 63;
-  const int64_t nw = (int64_t)gridDim.x * 4;
   const int D = g.D, DT = g.DT, DTp = g.DTp;
-  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < B; r += nw) {
-    const float gl = gld[r];
-    for (int j = lane; j < D; j += 64) {
-      const int i = fq[j];
-      const float v = gout[r * D + j];
-      float gi = v;
-      if (i < DT) {
-        const float e = Os ? expf(Os[r * DTp + i]) : 1.f;
-        if (Gs) Gs[r * DTp + i] = __fadd_rn(__fmul_rn(__fmul_rn(v, X[r * g.Dp + g.Cp + i]), e), gl);
-        if (Gt) Gt[r * DTp + i] = v;
-        gi = __fmul_rn(v, e);
+  int ii[kNJ];
+#pragma unroll
+  for (int q = 0; q < kNJ; ++q) ii[q] = lane + 64 * q < D ? fq[lane + 64 * q] : 0;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t r0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * kRU; r0 < B; r0 += nw * kRU) {
+    float vo[kRU][kNJ], xt[kRU][kNJ], sv[kRU][kNJ], gp[kRU][kNJ], gl[kRU];
+#pragma unroll
+    for (int u = 0; u < kRU; ++u) {
+      const int64_t r = r0 + u < B ? r0 + u : B - 1;  // past-the-end rows: loads only
+      gl[u] = gld[r];
+#pragma unroll
+      for (int q = 0; q < kNJ; ++q) {
+        const int j = lane + 64 * q, i = ii[q];
+        vo[u][q] = xt[u][q] = sv[u][q] = gp[u][q] = 0.f;
+        if (j < D) {
+          vo[u][q] = gout[r * D + j];
+          if (i < DT) {
+            xt[u][q] = X[r * g.Dp + g.Cp + i];
+            if (Os) sv[u][q] = Os[r * DTp + i];
+          }
+          if (gprev) gp[u][q] = gprev[r * D + i];
+        }
       }
-      if (gprev) gi += gprev[r * D + i];
-      gin[r * D + i] = gi;
     }
-    for (int i = DT + lane; i < DTp; i += 64) {
-      if (Gs) Gs[r * DTp + i] = 0.f;
-      if (Gt) Gt[r * DTp + i] = 0.f;
+#pragma unroll
+    for (int u = 0; u < kRU; ++u) {
+      const int64_t r = r0 + u;
+      if (r >= B) break;
+#pragma unroll
+      for (int q = 0; q < kNJ; ++q) {
+        const int j = lane + 64 * q, i = ii[q];
+        if (j >= D) continue;
+        const float v = vo[u][q];
+        float gi = v;
+        if (i < DT) {
+          const float e = Os ? expf(sv[u][q]) : 1.f;
+          if (Gs) Gs[r * DTp + i] = __fadd_rn(__fmul_rn(__fmul_rn(v, xt[u][q]), e), gl[u]);
+          if (Gt) Gt[r * DTp + i] = v;
+          gi = __fmul_rn(v, e);
+        }
+        if (gprev) gi += gp[u][q];
+        gin[r * D + i] = gi;
+      }
+      for (int i = DT + lane; i < DTp; i += 64) {
+        if (Gs) Gs[r * DTp + i] = 0.f;
+        if (Gt) Gt[r * DTp + i] = 0.f;
+      }
     }
   }
 }
@@ -520,8 +596,10 @@ __global__ __launch_bounds__(256) void k_wbwd_update(
 // z natural -> stash layout of the first inverse step's gathered input
 // z'[j] = z[iq[j]] (flip and rev_perm undone, flows/flows.py:115-117)
 __global__ __launch_bounds__(256) void k_winv_stash(const float* __restrict__ z,
-                                                    const int32_t* __restrict__ iq,
+                                                    const int32_t* __restrict__ iqg,
                                                     float* __restrict__ xs, int64_t B, Geo g) {
+  __shared__ int32_t sq[CNF_MAX_DIM];
+  const int32_t* iq = stage_table(sq, iqg, g.D);
   const int lane = threadIdx.x & 63;
   const int64_t nw = (int64_t)gridDim.x * 4;
   for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < B; r += nw) {
@@ -537,8 +615,10 @@ __global__ __launch_bounds__(256) void k_winv_fwd_update(const float* __restrict
                                                          float* __restrict__ Xn,
                                                          const float* __restrict__ Os,
                                                          const float* __restrict__ Ot,
-                                                         const int32_t* __restrict__ iqn,
+                                                         const int32_t* __restrict__ iqg,
                                                          int64_t B, Geo g) {
+  __shared__ int32_t sq[CNF_MAX_DIM];
+  const int32_t* iqn = stage_table(sq, iqg, g.D);
   const int lane = threadIdx.x & 63;
   const int64_t nw = (int64_t)gridDim.x * 4;
   for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < B; r += nw) {
@@ -596,9 +676,11 @@ __global__ __launch_bounds__(256) void k_winv_bwd_update(
 __global__ __launch_bounds__(256) void k_winv_scatter(const float* __restrict__ tmp,
                                                       float* __restrict__ out,
                                                       const float* __restrict__ gprev,
-                                                      const int32_t* __restrict__ iq, int64_t B,
+                                                      const int32_t* __restrict__ iqg, int64_t B,
                                                       int D, int skip) {
   if (skip) return;
+  __shared__ int32_t sq[CNF_MAX_DIM];
+  const int32_t* iq = stage_table(sq, iqg, D);
   const int lane = threadIdx.x & 63;
   const int64_t nw = (int64_t)gridDim.x * 4;
   for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < B; r += nw) {
