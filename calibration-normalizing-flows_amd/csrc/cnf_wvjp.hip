@@ -386,8 +386,10 @@ __global__ __launch_bounds__(256) void k_wstash(const float* __restrict__ x,
 // A wave takes kRU rows at a time and issues every load of the group before
 // the first use (lane l: columns j = l + 64q), so a wave has kRU rows of
 // loads in flight instead of one row's dependent round trips.
-constexpr int kRU = 4;                   // rows per wave per group
-constexpr int kNJ = CNF_MAX_DIM / 64;    // column slots per lane
+constexpr int kRU = 4;  // rows per wave per group
+// kNJ = column slots per lane, ceil(D / 64) (a template parameter, so the
+// register arrays are only as wide as the row)
+template <int kNJ>
 __global__ __launch_bounds__(256) void k_wfwd_update(const float* __restrict__ X,
                                                      float* __restrict__ Xn, float* __restrict__ ld,
                                                      const float* __restrict__ Os,
@@ -531,6 +533,7 @@ __global__ __launch_bounds__(256) void k_wseed(const float* __restrict__ Z,
 //   g_in_C = g_pre_C (the conditioners' share is added by the first Linear's
 //   back-prop), plus the caller's gradient of the previous layer's output.
 // kRU rows per wave with every load of the group issued first (as k_wfwd_update).
+template <int kNJ>
 __global__ __launch_bounds__(256) void k_wbwd_update(
     const float* __restrict__ gout, float* __restrict__ gin, const float* __restrict__ X,
     const float* __restrict__ Os, const float* __restrict__ gld, float* __restrict__ Gs,
@@ -694,6 +697,12 @@ __global__ __launch_bounds__(256) void k_winv_scatter(const float* __restrict__ 
 }
 
 inline int64_t al64(int64_t floats) { return (floats + 63) / 64 * 64; }
+
+// the instantiation whose column slots per lane cover D
+template <class F>
+F pick_nj(int D, F f1, F f2, F f3, F f4) {
+  return D <= 64 ? f1 : (D <= 128 ? f2 : (D <= 192 ? f3 : f4));
+}
 
 int lin_out(const Shape& s, int k) { return k == s.n_lin - 1 ? s.DT : s.units[k + 1]; }
 int lin_in(const Shape& s, int k) { return k == 0 ? s.DC : s.units[k]; }
@@ -1036,7 +1045,9 @@ int wvjp_run(const Shape& s, const void* prepared, const float* x, const int64_t
   hipLaunchKernelGGL(k_wstash, dim3(R.wave_blocks), dim3(256), 0, st, x, R.Xs(0), B, R.geom);
   for (int l = 0; l < L; ++l) {
     if (s.nets) R.nets_forward(l, l);
-    hipLaunchKernelGGL(k_wfwd_update, dim3(R.wave_blocks), dim3(256), 0, st, R.Xs(l), R.Xs(l + 1),
+    hipLaunchKernelGGL(pick_nj(D, k_wfwd_update<1>, k_wfwd_update<2>, k_wfwd_update<3>,
+                               k_wfwd_update<4>),
+                       dim3(R.wave_blocks), dim3(256), 0, st, R.Xs(l), R.Xs(l + 1),
                        ld, R.Os(l), R.Ot(l), fq + l * D, B, R.geom, l == 0);
   }
   // ---- seed ----
@@ -1055,7 +1066,9 @@ int wvjp_run(const Shape& s, const void* prepared, const float* x, const int64_t
     float* gin = (l == 0 && dx) ? dx : g[cur ^ 1];
     float* Gs = s.scale ? R.Gk(0, NL - 1) : nullptr;
     float* Gt = s.shift ? R.Gk(s.scale, NL - 1) : nullptr;
-    hipLaunchKernelGGL(k_wbwd_update, dim3(R.wave_blocks), dim3(256), 0, st, g[cur], gin, R.Xs(l),
+    hipLaunchKernelGGL(pick_nj(D, k_wbwd_update<1>, k_wbwd_update<2>, k_wbwd_update<3>,
+                               k_wbwd_update<4>),
+                       dim3(R.wave_blocks), dim3(256), 0, st, g[cur], gin, R.Xs(l),
                        R.Os(l), gld, Gs, Gt,
                        gz_all && l > 0 ? gz_all + (int64_t)(l - 1) * B * D : nullptr, fq + l * D,
                        B, R.geom);
