@@ -769,7 +769,7 @@ Plan make_plan(const Shape& s, int64_t B) {
   }
   for (int n = 0; n < s.nets; ++n)
     for (int k = 0; k < s.n_lin; ++k) p.G[n][k] = take(Bn * gp(s, k));
-  p.nseed = std::min<int64_t>(1024, (Bn + 15) / 16);
+  p.nseed = std::min<int64_t>(4096, (Bn + 15) / 16);  // one wave per row: 16 rows per wave at 2^18
   p.seed = take(p.nseed * 4);
   int64_t rows = (Bn + 255) / 256;
   rows = std::max<int64_t>(256, (rows + 31) / 32 * 32);
