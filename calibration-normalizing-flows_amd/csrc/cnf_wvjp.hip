@@ -180,6 +180,24 @@ __global__ __launch_bounds__(256, PAIR ? 3 : 4) void k_wgemm(GemmArgs ga) {
   __syncthreads();
   const int64_t M = ga.M, panels = (M + 31) >> 5, stride = (int64_t)gridDim.x * 4;
   auto epilogue = [&](const f16v (&acc)[4], int64_t m0) {
+    // the epilogue's operands (relu' source h, or the C being added to) are
+    // all loaded before the first store: j.mask / j.C may alias the output as
+    // far as the compiler knows, so loads interleaved with the stores would
+    // each pay a full memory round trip
+    float pre[NC][16];
+    if constexpr (EPI == kEpiMask || EPI == kEpiAdd) {
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int n = n0 + c * 32 + r;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int64_t m = m0 + (q & 3) + 8 * (q >> 2) + 4 * h;
+          const bool ok = m < M && (EPI == kEpiMask ? n < N : n < j.ldw);
+          pre[c][q] = 0.f;
+          if (ok) pre[c][q] = EPI == kEpiMask ? j.mask[m * j.ldm + n] : j.C[m * j.ldc + n];
+        }
+      }
+    }
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       const int n = n0 + c * 32 + r;
@@ -198,11 +216,11 @@ __global__ __launch_bounds__(256, PAIR ? 3 : 4) void k_wgemm(GemmArgs ga) {
           else v = v < 0.f ? 0.f : v;  // keeps NaN (torch relu)
         }
         if constexpr (EPI == kEpiMask) {  // its derivative from the stored output h
-          const float h = real ? j.mask[m * j.ldm + n] : 0.f;
+          const float h = pre[c][q];
           v = j.act == 2 ? v * (1.f - h * h) : (h > 0.f ? v : 0.f);
           if (!real) v = 0.f;
         }
-        if constexpr (EPI == kEpiAdd) v += j.C[m * j.ldc + n];
+        if constexpr (EPI == kEpiAdd) v += pre[c][q];
         j.C[m * j.ldc + n] = real ? v : pad;
       }
     }
