@@ -179,6 +179,15 @@ __global__ __launch_bounds__(256, PAIR ? 3 : 4) void k_wgemm(GemmArgs ga) {
   }
   __syncthreads();
   const int64_t M = ga.M, panels = (M + 31) >> 5, stride = (int64_t)gridDim.x * 4;
+  // a lane's output columns are fixed for the whole launch: its biases are
+  // loaded once, not after each panel's stores (j.bias may alias j.C as far as
+  // the compiler knows, which would hold every panel's bias load behind them)
+  float bias_c[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int n = n0 + c * 32 + r;
+    bias_c[c] = (EPI == kEpiBias || EPI == kEpiBiasRelu) && n < N ? j.bias[n] : 0.f;
+  }
   auto epilogue = [&](const f16v (&acc)[4], int64_t m0) {
     // the epilogue's operands (relu' source h, or the C being added to) are
     // all loaded before the first store: j.mask / j.C may alias the output as
@@ -204,7 +213,7 @@ __global__ __launch_bounds__(256, PAIR ? 3 : 4) void k_wgemm(GemmArgs ga) {
       if (n >= j.ldw) continue;
       const bool real = n < N;
       const float pad = (j.ones && n == N) ? 1.f : 0.f;
-      const float b = (EPI == kEpiBias || EPI == kEpiBiasRelu) && real ? j.bias[n] : 0.f;
+      const float b = bias_c[c];
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int64_t m = m0 + (q & 3) + 8 * (q >> 2) + 4 * h;
