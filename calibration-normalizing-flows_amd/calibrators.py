@@ -93,6 +93,22 @@ def _native_stack(flow, dev, need_vjp=True):
     return stack if st == 0 else None
 
 
+def _loader_order(n):
+    """The row order of one pass of DataLoader(TensorDataset(...), batch_size,
+    shuffle=True) (calibrators.py:274-275) with torch's global CPU RNG in the
+    same state: creating the loader iterator draws its base seed
+    (torch.utils.data._BaseDataLoaderIter), then the RandomSampler draws the
+    seed of a fresh CPU generator and takes randperm(n) from it.  Both draws
+    are reproduced, so the global RNG advances exactly as in the reference.
+    Returns a pinned int64 CPU tensor (one async H2D per pass)."""
+    torch.empty((), dtype=torch.int64).random_()  # the iterator's _base_seed
+    seed = int(torch.empty((), dtype=torch.int64).random_().item())
+    g = torch.Generator()
+    g.manual_seed(seed)
+    order = torch.randperm(n, generator=g)
+    return order.pin_memory() if torch.cuda.is_available() else order
+
+
 class TorchFlowCalibrator(Calibrator):
     """Trains a normalizing flow on (logits, target) by minimising
     -mean(log(softmax(f(x))[y] + 1e-7) + log|det J_f(x)|)  (calibrators.py:239-353)."""
@@ -164,40 +180,43 @@ class TorchFlowCalibrator(Calibrator):
         return history
 
     def _fit_native(self, stack, logits, target, epochs, batch_size):
-        """Same schedule on the fused kernels: one cnf_loss_vjp launch per
-        training batch, one cnf_forward_loss launch per evaluation batch."""
+        """Same schedule on the fused kernels: one cnf_loss_vjp launch plus one
+        cnf_adam_step launch per training batch, one cnf_forward_loss launch per
+        evaluation batch.  Each pass over the data draws its order exactly as
+        the reference's DataLoader(shuffle=True) does (_loader_order), so
+        minibatch runs see the reference's batches and the eval history keeps
+        the reference's last-batch value (calibrators.py:274-317)."""
         from cnf_hip import vjp as V
         from cnf_hip.adam import StackAdam
-        # the optimizer step on the device in one launch (the torch Adam's
-        # hyper-parameters), straight from the fused step's flat gradient
-        adam = getattr(self, "_stack_adam", None)
-        if adam is None or adam.stack is not stack:
-            adam = StackAdam.like(stack, self.optimizer)
-            self._stack_adam = adam
+        # the optimizer step on the device in one launch, with the torch Adam's
+        # current hyper-parameters and state (written back after the fit)
+        adam = StackAdam.like(stack, self.optimizer)
         N = logits.shape[0]
+        bs = max(1, int(batch_size))
         history = {'loss': [], 'ce': [], 'log_det': []}
-        gen = torch.Generator(device=logits.device)
-        gen.manual_seed(int(torch.randint(0, 2 ** 62, (1,)).item()))
+        dev = logits.device
+
+        def batches():
+            # one gather of the permuted rows per pass; batches are views
+            order = _loader_order(N).to(dev, non_blocking=True)
+            xs, ys = logits.index_select(0, order), target.index_select(0, order)
+            return [(xs[s:s + bs], ys[s:s + bs]) for s in range(0, N, bs)]
+
         for epoch in range(epochs):
             self.flow.train()
-            order = torch.randperm(N, device=logits.device, generator=gen)  # shuffle=True
-            for s in range(0, N, batch_size):
-                idx = order[s:s + batch_size]
-                xb, yb = logits.index_select(0, idx), target.index_select(0, idx)
+            for xb, yb in batches():
                 _, grads, _ = V.loss_and_grads(stack, xb, yb, grad_scale=1.0 / xb.shape[0])
                 adam.step(grads)
             self.flow.eval()
-            order = torch.randperm(N, device=logits.device, generator=gen)
             num = 0
             terms = None
-            for s in range(0, N, batch_size):
-                idx = order[s:s + batch_size]
-                terms, _, _ = stack.forward_loss(logits.index_select(0, idx),
-                                                 target.index_select(0, idx))
-                num += idx.numel()
+            for xb, yb in batches():
+                terms, _, _ = stack.forward_loss(xb, yb)
+                num += xb.shape[0]
             history['loss'].append(terms[0] / num)
             history['ce'].append(terms[1] / num)
             history['log_det'].append(terms[2] / num)
+        adam.store_into(self.optimizer)
         return history
 
     # -------------------------------------------------------------- predict

@@ -15,7 +15,7 @@ import torch  # noqa: F401  (load torch's HIP runtime before ours)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CNF_HIP_LIB", os.path.join(_HERE, "libcnf_hip.so"))
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 MAX_HIDDEN = 8
 MAX_DIM = 256
 LOSS_CAL = 0
@@ -69,7 +69,8 @@ _lock = threading.Lock()
 
 
 def _bind(lib):
-    P, I32, I64, F = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_float
+    P, I32, I64, F, DB = (ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_float,
+                          ctypes.c_double)
     D = ctypes.POINTER(CnfDesc)
     sig = {
         "cnf_param_count": (ctypes.c_int, [D, ctypes.POINTER(I64)]),
@@ -90,7 +91,8 @@ def _bind(lib):
         "cnf_vjp_inverse_workspace_bytes": (ctypes.c_int,
                                             [D, I64, ctypes.POINTER(ctypes.c_size_t)]),
         "cnf_vjp_inverse": (ctypes.c_int, [D, P, P, P, P, P, P, P, I64, P, ctypes.c_size_t, P]),
-        "cnf_adam_step": (ctypes.c_int, [D, ctypes.POINTER(P), P, P, P, I64, F, F, F, F, F, P]),
+        "cnf_adam_step": (ctypes.c_int, [D, ctypes.POINTER(P), P, P, P, I64, DB, DB, DB, DB, DB,
+                                         P]),
         "cnf_kernel_name": (ctypes.c_char_p, [D]),
         "cnf_strerror": (ctypes.c_char_p, [ctypes.c_int]),
         "cnf_last_hip_error": (ctypes.c_int, []),

@@ -2,7 +2,14 @@
 (cnf_adam_step, include/cnf.h), fed by the flat gradient of cnf_loss_vjp:
 the optimizer half of the calibrator's fused training step (SURVEY 8(f) rank 1;
 the reference steps torch.optim.Adam at its defaults, calibrators.py:239-295).
-Same update as torch.optim.Adam (amsgrad off)."""
+Same update as torch.optim.Adam (amsgrad off), with torch's scalar rounding
+(the hyper-parameters cross the ABI as doubles).
+
+`StackAdam.like(stack, torch_adam)` takes the torch optimizer's CURRENT
+hyper-parameters and, when it already holds state for the stack's parameters
+(an earlier fit), its step count and moments; `store_into(torch_adam)` writes
+the state back, so the torch optimizer and the native one never diverge
+across fit() calls."""
 import ctypes
 
 import torch
@@ -16,17 +23,51 @@ class StackAdam:
 
     def __init__(self, stack, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
         self.stack = stack
-        self.lr, self.betas, self.eps, self.weight_decay = lr, tuple(betas), eps, weight_decay
+        self.lr, self.betas, self.eps, self.weight_decay = (float(lr), tuple(map(float, betas)),
+                                                            float(eps), float(weight_decay))
         self.t = 0
         self._m = self._v = None
 
     @classmethod
     def like(cls, stack, torch_adam):
-        """Hyper-parameters of an existing torch.optim.Adam (first group)."""
-        g = torch_adam.param_groups[0]
+        """Hyper-parameters (and state, if any) of an existing torch.optim.Adam.
+        Every stack parameter must sit in one param group."""
+        ps = stack.param_tensors()
+        ids = {id(p) for p in ps}
+        groups = [g for g in torch_adam.param_groups if any(id(p) in ids for p in g["params"])]
+        if len(groups) != 1:
+            raise ValueError("StackAdam: the stack's parameters must share one param group")
+        g = groups[0]
         if g.get("amsgrad") or g.get("maximize"):
             raise ValueError("StackAdam: amsgrad / maximize are not supported")
-        return cls(stack, g["lr"], g["betas"], g["eps"], g["weight_decay"])
+        lr = g["lr"].item() if torch.is_tensor(g["lr"]) else g["lr"]
+        self = cls(stack, lr, g["betas"], g["eps"], g["weight_decay"])
+        st = [torch_adam.state.get(p) for p in ps]
+        if all(s is not None and "exp_avg" in s for s in st):
+            steps = {int(s["step"]) for s in st}
+            if len(steps) != 1:
+                raise ValueError("StackAdam: parameters at different step counts")
+            self.t = steps.pop()
+            dev = ps[0].device
+            self._m = torch.cat([s["exp_avg"].reshape(-1).to(dev, torch.float32) for s in st])
+            self._v = torch.cat([s["exp_avg_sq"].reshape(-1).to(dev, torch.float32) for s in st])
+        return self
+
+    def store_into(self, torch_adam):
+        """Write step count and moments into the torch optimizer's state (the
+        layout torch.optim.Adam keeps: per parameter, a 0-d float32 `step` and
+        moments shaped like the parameter)."""
+        if self._m is None:
+            return
+        off = 0
+        for p in self.stack.param_tensors():
+            n = p.numel()
+            torch_adam.state[p] = {
+                "step": torch.tensor(float(self.t), dtype=torch.float32),
+                "exp_avg": self._m[off:off + n].view_as(p).clone(),
+                "exp_avg_sq": self._v[off:off + n].view_as(p).clone(),
+            }
+            off += n
 
     def step(self, flat_grads):
         ps = self.stack.param_tensors()
@@ -35,6 +76,8 @@ class StackAdam:
             n = self.stack.param_count()
             self._m = torch.zeros(n, dtype=torch.float32, device=dev)
             self._v = torch.zeros(n, dtype=torch.float32, device=dev)
+        elif self._m.device != dev:
+            self._m, self._v = self._m.to(dev), self._v.to(dev)
         for p in ps:
             if not p.is_contiguous():
                 raise ValueError("StackAdam needs contiguous parameters")
@@ -42,9 +85,9 @@ class StackAdam:
         arr = (ctypes.c_void_p * len(ps))(*[p.data_ptr() for p in ps])
         lib = _lib.lib()
         st = lib.cnf_adam_step(ctypes.byref(self.stack.desc), arr, _ptr(flat_grads), _ptr(self._m),
-                               _ptr(self._v), ctypes.c_int64(self.t), ctypes.c_float(self.lr),
-                               ctypes.c_float(self.betas[0]), ctypes.c_float(self.betas[1]),
-                               ctypes.c_float(self.eps), ctypes.c_float(self.weight_decay),
+                               _ptr(self._v), ctypes.c_int64(self.t), ctypes.c_double(self.lr),
+                               ctypes.c_double(self.betas[0]), ctypes.c_double(self.betas[1]),
+                               ctypes.c_double(self.eps), ctypes.c_double(self.weight_decay),
                                _stream(dev))
         _lib.check("cnf_adam_step", st)
         # the kernel wrote the parameters behind autograd's back: bump their

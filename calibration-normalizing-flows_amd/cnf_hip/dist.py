@@ -7,8 +7,22 @@ one flat buffer per step with a single all-reduce (RCCL over xGMI when the
 process group is "nccl"; gloo for the CPU tests):
 
   train step  [grad_scale * d(sum of shard loss)/dW  (P floats) | loss terms (3)]
-              -> all_reduce(SUM) -> optimizer.step() on identical replicas
+              -> all_reduce(SUM) -> Adam step on identical replicas
   eval        [loss terms (3)] -> all_reduce(SUM)
+
+On a ROCm device the step is three launches and one collective, no host
+sync: cnf_loss_vjp on the shard, the all-reduce of the flat buffer, and
+cnf_adam_step (the calibrator's optimizer, calibrators.py:259, 295) reading the
+reduced gradient in place.  The torch optimizer handed to the trainer supplies
+the hyper-parameters and, through sync_optimizer(), receives the state.
+
+Overlap: the all-reduce cannot run under the next step's forward (that
+forward needs the updated weights); overlapping it with the reverse mode
+would need per-layer buckets of the layer-at-a-time wide VJP.  At cfg4
+(727,200 floats = 2.9 MB per step) a ring all-reduce over 8 ranks moves
+2 * 7/8 * 2.9 MB per rank, about 40 us at 7 x 153 GB/s of xGMI even before
+latency terms, against a ~25 ms step: under 0.5 %, so one bucket at the end
+of the step ships.
 
 grad_scale = 1 / global batch, so the summed gradient is exactly the gradient
 of the reference's -mean over the whole (unsharded) batch.  For cfg2
@@ -72,6 +86,7 @@ class ShardedFlowTrainer:
         self.optimizer = optimizer
         self.group = group
         self.params = list(_coupling_params(flow))
+        self._adam = None  # StackAdam of the native path (built on the first step)
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         if broadcast and self.world > 1:
             # every replica starts from rank 0's state (weights, masks, permutations)
@@ -85,6 +100,22 @@ class ShardedFlowTrainer:
     def step(self, x, y, global_batch, kind=_lib.LOSS_CAL, det=1.0):
         """One synchronous step on this rank's shard; returns the global
         (loss, ce, log-det) sums as a device tensor (no host sync)."""
+        stack = _native(self.flow, x)
+        if stack is not None:
+            from .vjp import loss_and_grads
+            from .adam import StackAdam
+            # one flat buffer [grads | terms]: the fused kernel writes both, the
+            # collective reduces both, Adam reads the gradient part in place
+            P = stack.param_count()
+            buf = torch.empty(P + 3, dtype=torch.float32, device=x.device)
+            loss_and_grads(stack, x, y, kind=kind, det=det, grad_scale=1.0 / global_batch,
+                           grads_out=buf[:P], terms_out=buf[P:])
+            if self.world > 1:
+                dist.all_reduce(buf, group=self.group)
+            if self._adam is None or self._adam.stack is not stack:
+                self._adam = StackAdam.like(stack, self.optimizer)
+            self._adam.step(buf[:P])
+            return buf[P:]
         grads, terms = local_loss_and_grads(self.flow, x, y, 1.0 / global_batch, kind, det)
         buf = torch.cat([grads, terms])
         if self.world > 1:
@@ -96,6 +127,12 @@ class ShardedFlowTrainer:
             off += n
         self.optimizer.step()
         return buf[off:off + 3]
+
+    def sync_optimizer(self):
+        """Write the native Adam's step count and moments into the torch
+        optimizer's state (no-op on the torch path, which steps it directly)."""
+        if self._adam is not None:
+            self._adam.store_into(self.optimizer)
 
     @torch.no_grad()
     def evaluate(self, x, y, kind=_lib.LOSS_CAL, det=1.0):

@@ -72,6 +72,7 @@ class CouplingStack:
         self._refresh_desc()
         self._cache = {}
         self._loss_ws = {}
+        self._vjp_ok = None
 
     # -- descriptor and permutations ----------------------------------------
     def _perm_tensors(self):
@@ -113,6 +114,17 @@ class CouplingStack:
         sgpr-fused stack run on valu-fused (cnf_valu.hip valu_run)."""
         name = _lib.lib().cnf_kernel_name(ctypes.byref(self.desc)).decode()
         return "valu-fused" if all_outputs and name == "sgpr-fused" else name
+
+    def has_native_vjp(self):
+        """True when cnf_vjp serves this descriptor (strict_nan stacks, for
+        one, have no native reverse mode).  Cached: support depends only on the
+        shape and options."""
+        if self._vjp_ok is None:
+            n = ctypes.c_size_t()
+            st = _lib.lib().cnf_vjp_workspace_bytes(ctypes.byref(self.desc), ctypes.c_int64(1),
+                                                    ctypes.byref(n))
+            self._vjp_ok = st == 0
+        return self._vjp_ok
 
     def param_tensors(self):
         """ABI order (include/cnf.h cnf_param_tensor_count)."""
@@ -272,10 +284,13 @@ class CouplingStack:
     # -------------------------------------------------------------- autograd
     def forward_autograd(self, x, want_all):
         """Forward with gradients w.r.t. x and every parameter (cnf_vjp): the
-        cnf::flow operator (autograd kernel in C++) or the Python Function."""
+        cnf::flow operator (autograd kernel in C++) or the Python Function.
+        Stacks without a native reverse mode (strict_nan) take the Python
+        Function, whose backward falls back to torch autograd (vjp._torch_vjp);
+        the C++ kernel would raise there."""
         ps = self.param_tensors()
         ops = _ops()
-        if ops is not None:
+        if ops is not None and self.has_native_vjp():
             x = self._check_input(x)
             blob = self.prepared(x.device)
             stats["forward"] += 1

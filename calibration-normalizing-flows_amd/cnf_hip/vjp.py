@@ -117,18 +117,26 @@ def stack_vjp_inverse(stack, z, g_out, g_ld, all_grads, need_dz, blob=None):
     return dz, _split(stack, grads)
 
 
-def loss_and_grads(stack, x, y, kind=_lib.LOSS_CAL, det=1.0, grad_scale=1.0, need_dx=False):
+def loss_and_grads(stack, x, y, kind=_lib.LOSS_CAL, det=1.0, grad_scale=1.0, need_dx=False,
+                   grads_out=None, terms_out=None):
     """Fused forward + loss + reverse mode.  Returns (terms[3], flat grads, dx)
     where terms = (sum of per-row loss, sum of ce, sum of log-det) over THIS
-    batch and grads = grad_scale * d(sum of per-row loss)/d(params)."""
+    batch and grads = grad_scale * d(sum of per-row loss)/d(params).
+    grads_out / terms_out: caller-provided contiguous fp32 destinations (e.g.
+    the two parts of one all-reduce buffer)."""
     x = x.contiguous()
     y = y.contiguous().to(torch.int64)
     B = x.shape[0]
     dev = x.device
     blob = stack.prepared(dev)
     ws, nws = _workspace(stack, B, dev)
-    grads = torch.empty(stack.param_count(), dtype=torch.float32, device=dev)
-    terms = torch.empty(3, dtype=torch.float32, device=dev)
+    grads = torch.empty(stack.param_count(), dtype=torch.float32, device=dev) \
+        if grads_out is None else grads_out
+    terms = torch.empty(3, dtype=torch.float32, device=dev) if terms_out is None else terms_out
+    for t, n in ((grads, stack.param_count()), (terms, 3)):
+        if t.numel() != n or not t.is_contiguous() or t.dtype != torch.float32 or t.device != dev:
+            raise ValueError("loss_and_grads: output buffer must be contiguous fp32 [%d] on %s"
+                             % (n, dev))
     dx = torch.empty_like(x) if need_dx else None
     lib = _lib.lib()
     st = lib.cnf_loss_vjp(ctypes.byref(stack.desc), _ptr(blob), _ptr(x), _ptr(y),
@@ -147,6 +155,10 @@ def _torch_vjp(stack, x, g_out, g_ld, all_grads, need_dx):
     """Shapes without a native VJP (strict-NaN mode, the MFMA-tile family):
     autograd through the layers' own torch ops, on the same device."""
     key = (stack.dim, tuple(stack.hidden), stack.strict_nan)
+    if stack.options & (_lib.OPT_ALT_MASK | _lib.OPT_S_TANH):
+        # _torch_forward restates the maintained (ReLU, data-flip) layer only:
+        # a legacy stack must not differentiate through it
+        raise _lib.UnsupportedShape("cnf_vjp", -3, _lib.lib())
     from flows.flows import STRICT_NATIVE
     if STRICT_NATIVE:
         raise RuntimeError("native coupling path unavailable: no native VJP for %s" % (key,))

@@ -28,7 +28,10 @@ struct AdamArgs {
   const float* g;
   float* m;
   float* v;
-  float beta1, beta2, eps, wd, step_size, bc2_sqrt;
+  // torch's scalars, each rounded to fp32 once: 1 - beta1 and 1 - beta2 are
+  // formed in double from the optimizer's Python floats (torch/optim/adam.py
+  // _single_tensor_adam: lerp_(grad, 1 - beta1), addcmul_(value=1 - beta2))
+  float omb1, beta2, omb2, eps, wd, step_size, bc2_sqrt;
 };
 
 __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
@@ -42,9 +45,9 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
     float g = a.g[f];
     if (a.wd != 0.f) g = __fadd_rn(g, __fmul_rn(a.wd, pv));            // grad.add(p, alpha=wd)
     float m = a.m[f];
-    m = __fadd_rn(m, __fmul_rn(1.f - a.beta1, __fsub_rn(g, m)));        // lerp_(g, 1 - beta1)
+    m = __fadd_rn(m, __fmul_rn(a.omb1, __fsub_rn(g, m)));              // lerp_(g, 1 - beta1)
     const float v = __fadd_rn(__fmul_rn(a.v[f], a.beta2),
-                              __fmul_rn(__fmul_rn(g, g), 1.f - a.beta2));  // mul_().addcmul_()
+                              __fmul_rn(__fmul_rn(g, g), a.omb2));         // mul_().addcmul_()
     a.m[f] = m;
     a.v[f] = v;
     const float denom = __fadd_rn(__fdiv_rn(sqrtf(v), a.bc2_sqrt), a.eps);
@@ -58,8 +61,8 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
 using namespace cnf;
 
 extern "C" int cnf_adam_step(const cnf_desc* desc, float* const* params, const float* grads,
-                             float* exp_avg, float* exp_avg_sq, int64_t step, float lr,
-                             float beta1, float beta2, float eps, float weight_decay,
+                             float* exp_avg, float* exp_avg_sq, int64_t step, double lr,
+                             double beta1, double beta2, double eps, double weight_decay,
                              void* stream) {
   Shape s;
   int st = derive_shape(desc, &s);
@@ -68,16 +71,17 @@ extern "C" int cnf_adam_step(const cnf_desc* desc, float* const* params, const f
   const int nt = s.L * s.nets * s.n_lin * 2;
   if (nt == 0) return CNF_OK;
   if (!params || !grads || !exp_avg || !exp_avg_sq) return CNF_ERR_NULL;
-  const double bc1 = 1.0 - std::pow((double)beta1, (double)step);
-  const double bc2 = 1.0 - std::pow((double)beta2, (double)step);
+  const double bc1 = 1.0 - std::pow(beta1, (double)step);
+  const double bc2 = 1.0 - std::pow(beta2, (double)step);
   AdamArgs a{};
   a.g = grads;
   a.m = exp_avg;
   a.v = exp_avg_sq;
-  a.beta1 = beta1;
-  a.beta2 = beta2;
-  a.eps = eps;
-  a.wd = weight_decay;
+  a.omb1 = (float)(1.0 - beta1);
+  a.beta2 = (float)beta2;
+  a.omb2 = (float)(1.0 - beta2);
+  a.eps = (float)eps;
+  a.wd = (float)weight_decay;
   a.step_size = (float)(lr / bc1);
   a.bc2_sqrt = (float)std::sqrt(bc2);
   // tensor sizes in ABI order: per layer, per net, per Linear: W then b

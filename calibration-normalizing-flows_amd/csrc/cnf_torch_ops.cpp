@@ -20,6 +20,7 @@
 // `desc` is the descriptor as integers: [dim, n_layers, n_hidden, hidden[0..7],
 // scale, shift, strict_nan, options]; `perms` an optional host int64 [L, D]
 // table (row[0] < 0: no permutation), as cnf_desc.perms.
+#include <c10/core/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
 #include <torch/library.h>
 #include <torch/torch.h>
@@ -65,7 +66,13 @@ void check(const char* fn, int st) {
               st == CNF_ERR_HIP ? " (hipError " + std::to_string(cnf_last_hip_error()) + ")" : "");
 }
 
-void* stream() { return (void*)c10::hip::getCurrentHIPStream().stream(); }
+// The current stream of x's device: the dispatcher sets no device guard for
+// these operators, so each one guards x's device itself (DevGuard below) and
+// launches on that device's current stream, as the ctypes path does.
+void* stream(const Tensor& x) {
+  return (void*)c10::hip::getCurrentHIPStream(x.device().index()).stream();
+}
+using DevGuard = c10::DeviceGuard;
 
 const float* fptr(const c10::optional<Tensor>& t) {
   return t.has_value() && t->defined() ? t->data_ptr<float>() : nullptr;
@@ -81,6 +88,7 @@ Tensor rows(const Tensor& x, const Desc& d) {
 std::tuple<Tensor, Tensor> forward_impl(const Tensor& x_, const Tensor& prepared,
                                         c10::IntArrayRef desc, const c10::optional<Tensor>& perms,
                                         bool inverse, bool all_outputs) {
+  DevGuard guard(x_.device());
   Desc d = make_desc(desc, perms);
   Tensor x = rows(x_, d);
   const int64_t B = x.size(0), D = d.d.dim, L = d.d.n_layers;
@@ -89,9 +97,9 @@ std::tuple<Tensor, Tensor> forward_impl(const Tensor& x_, const Tensor& prepared
   float* fin = all_outputs ? nullptr : out.data_ptr<float>();
   float* all = all_outputs ? out.data_ptr<float>() : nullptr;
   const int st = inverse ? cnf_inverse(&d.d, prepared.data_ptr(), x.data_ptr<float>(), fin,
-                                       ld.data_ptr<float>(), all, B, stream())
+                                       ld.data_ptr<float>(), all, B, stream(x))
                          : cnf_forward(&d.d, prepared.data_ptr(), x.data_ptr<float>(), fin,
-                                       ld.data_ptr<float>(), all, B, stream());
+                                       ld.data_ptr<float>(), all, B, stream(x));
   check(inverse ? "cnf_inverse" : "cnf_forward", st);
   return {out, ld};
 }
@@ -99,6 +107,7 @@ std::tuple<Tensor, Tensor> forward_impl(const Tensor& x_, const Tensor& prepared
 Tensor forward_loss_impl(const Tensor& x_, const Tensor& y_, const Tensor& prepared,
                          c10::IntArrayRef desc, const c10::optional<Tensor>& perms, int64_t kind,
                          double det) {
+  DevGuard guard(x_.device());
   Desc d = make_desc(desc, perms);
   Tensor x = rows(x_, d);
   Tensor y = y_.to(torch::kInt64).contiguous();
@@ -110,7 +119,7 @@ Tensor forward_loss_impl(const Tensor& x_, const Tensor& y_, const Tensor& prepa
   check("cnf_forward_loss",
         cnf_forward_loss(&d.d, prepared.data_ptr(), x.data_ptr<float>(), y.data_ptr<int64_t>(),
                          (int32_t)kind, (float)det, nullptr, nullptr, terms.data_ptr<float>(), B,
-                         ws.data_ptr(), n, stream()));
+                         ws.data_ptr(), n, stream(x)));
   return terms;
 }
 
@@ -129,6 +138,7 @@ std::tuple<Tensor, Tensor> loss_and_grads_impl(const Tensor& x_, const Tensor& y
                                                const Tensor& prepared, c10::IntArrayRef desc,
                                                const c10::optional<Tensor>& perms, int64_t kind,
                                                double det, double grad_scale) {
+  DevGuard guard(x_.device());
   Desc d = make_desc(desc, perms);
   Tensor x = rows(x_, d);
   Tensor y = y_.to(torch::kInt64).contiguous();
@@ -140,7 +150,7 @@ std::tuple<Tensor, Tensor> loss_and_grads_impl(const Tensor& x_, const Tensor& y
   check("cnf_loss_vjp",
         cnf_loss_vjp(&d.d, prepared.data_ptr(), x.data_ptr<float>(), y.data_ptr<int64_t>(),
                      (int32_t)kind, (float)det, (float)grad_scale, terms.data_ptr<float>(),
-                     grads.data_ptr<float>(), nullptr, B, ws.data_ptr(), n, stream()));
+                     grads.data_ptr<float>(), nullptr, B, ws.data_ptr(), n, stream(x)));
   return {terms, grads};
 }
 
@@ -149,6 +159,7 @@ std::tuple<Tensor, Tensor> vjp_impl(const Tensor& x_, const Tensor& prepared,
                                     const c10::optional<Tensor>& gz,
                                     const c10::optional<Tensor>& gz_all,
                                     const c10::optional<Tensor>& gld, bool need_dx) {
+  DevGuard guard(x_.device());
   Desc d = make_desc(desc, perms);
   Tensor x = rows(x_, d);
   const int64_t B = x.size(0);
@@ -165,12 +176,13 @@ std::tuple<Tensor, Tensor> vjp_impl(const Tensor& x_, const Tensor& prepared,
   check("cnf_vjp", cnf_vjp(&d.d, prepared.data_ptr(), x.data_ptr<float>(), fptr(g1), fptr(g2),
                            fptr(g3), grads.data_ptr<float>(),
                            need_dx ? dx.data_ptr<float>() : nullptr, B, ws.data_ptr(), n,
-                           stream()));
+                           stream(x)));
   return {grads, dx};
 }
 
 Tensor predict_impl(const Tensor& x_, const Tensor& prepared, c10::IntArrayRef desc,
                     const c10::optional<Tensor>& perms, const Tensor& log_priors) {
+  DevGuard guard(x_.device());
   Desc d = make_desc(desc, perms);
   Tensor x = rows(x_, d);
   Tensor lp = log_priors.to(x.device(), torch::kFloat32).contiguous();
@@ -178,7 +190,7 @@ Tensor predict_impl(const Tensor& x_, const Tensor& prepared, c10::IntArrayRef d
   Tensor probs = torch::empty_like(x);
   check("cnf_predict", cnf_predict(&d.d, prepared.data_ptr(), x.data_ptr<float>(),
                                    lp.data_ptr<float>(), probs.data_ptr<float>(), nullptr,
-                                   x.size(0), stream()));
+                                   x.size(0), stream(x)));
   return probs;
 }
 

@@ -56,6 +56,27 @@ from torch import nn
 
 from .utils import MLP
 
+
+class UnsupportedShape(Exception):
+    """Stand-in until the native library is imported (CPU-only use)."""
+
+
+def _not_native(why):
+    from .flows import _not_native as nn_
+    nn_(why)
+
+
+def _bind_unsupported():
+    global UnsupportedShape
+    try:
+        from cnf_hip._lib import UnsupportedShape as U
+        UnsupportedShape = U
+    except ImportError:
+        pass
+
+
+_bind_unsupported()
+
 _ACT = {"relu": F.relu, "tanh": torch.tanh}
 
 
@@ -142,12 +163,17 @@ class LegacyRealNvpFlow(nn.Module):
 
     def forward(self, x):
         if self._native_ok(x):
-            stack = self._native_stack()
-            if torch.is_grad_enabled() and (x.requires_grad or stack.requires_grad()):
-                y, ld = stack.forward_autograd(x, want_all=False)
-            else:
+            try:
+                stack = self._native_stack()
+                if torch.is_grad_enabled() and (x.requires_grad or stack.requires_grad()):
+                    if not stack.has_native_vjp():
+                        # the torch VJP restates the maintained layer only
+                        raise UnsupportedShape("cnf_vjp", -3, __import__("cnf_hip").lib())
+                    return stack.forward_autograd(x, want_all=False)
                 y, ld, _ = stack.run(x)
-            return y, ld
+                return y, ld
+            except UnsupportedShape as e:
+                _not_native("legacy RealNVP %s" % e)
         ld = torch.zeros(x.shape[0], dtype=x.dtype, device=x.device)
         for ly in self.layers:
             x, l = ly(x)
@@ -156,11 +182,14 @@ class LegacyRealNvpFlow(nn.Module):
 
     def backward(self, y):
         if self._native_ok(y):
-            stack = self._native_stack()
-            if torch.is_grad_enabled() and (y.requires_grad or stack.requires_grad()):
-                return stack.inverse_autograd(y, want_all=False)  # cnf_vjp_inverse
-            x, ld, _ = stack.run(y, inverse=True)
-            return x, ld
+            try:
+                stack = self._native_stack()
+                if torch.is_grad_enabled() and (y.requires_grad or stack.requires_grad()):
+                    return stack.inverse_autograd(y, want_all=False)  # cnf_vjp_inverse
+                x, ld, _ = stack.run(y, inverse=True)
+                return x, ld
+            except UnsupportedShape as e:
+                _not_native("legacy RealNVP %s" % e)
         ld = torch.zeros(y.shape[0], dtype=y.dtype, device=y.device)
         for ly in reversed(self.layers):
             y, l = ly.backward(y)
@@ -313,11 +342,17 @@ class LegacyNiceFlow(nn.Module):
 
     def forward(self, x):
         if self._native_ok(x):
-            stack = self._native_stack()
-            if torch.is_grad_enabled() and (x.requires_grad or stack.requires_grad()):
-                return stack.forward_autograd(x, want_all=False)
-            y, ld, _ = stack.run(x)
-            return y, ld
+            try:
+                stack = self._native_stack()
+                if torch.is_grad_enabled() and (x.requires_grad or stack.requires_grad()):
+                    if not stack.has_native_vjp():
+                        # the torch VJP restates the maintained layer only
+                        raise UnsupportedShape("cnf_vjp", -3, __import__("cnf_hip").lib())
+                    return stack.forward_autograd(x, want_all=False)
+                y, ld, _ = stack.run(x)
+                return y, ld
+            except UnsupportedShape as e:
+                _not_native("legacy NICE %s" % e)
         ld = torch.zeros(x.shape[0], dtype=x.dtype, device=x.device)
         for ly in self.layers:
             x = ly(x)[0] if self.version == 3 else ly(x)
@@ -329,11 +364,14 @@ class LegacyNiceFlow(nn.Module):
 
     def backward(self, y):
         if self._native_ok(y):
-            stack = self._native_stack()
-            if torch.is_grad_enabled() and (y.requires_grad or stack.requires_grad()):
-                return stack.inverse_autograd(y, want_all=False)
-            x, ld, _ = stack.run(y, inverse=True)
-            return x, ld
+            try:
+                stack = self._native_stack()
+                if torch.is_grad_enabled() and (y.requires_grad or stack.requires_grad()):
+                    return stack.inverse_autograd(y, want_all=False)
+                x, ld, _ = stack.run(y, inverse=True)
+                return x, ld
+            except UnsupportedShape as e:
+                _not_native("legacy NICE %s" % e)
         ld = torch.zeros(y.shape[0], dtype=y.dtype, device=y.device)
         if self.version == 2 and len(self.layers) % 2 == 1:
             y = self._rev(y)

@@ -36,8 +36,13 @@ class RealNvpFlow(CouplingFlow):
             if mask_mode != "alternate_mask":
                 raise ValueError("s_activation='tanh' is the legacy flow: "
                                  "use it with mask_mode='alternate_mask'")
+            # code-old/realNVP.py:58-64: the s-net is always tanh there
+            s_act = "tanh" if s_activation in (None, "tanh") else s_activation
+            if s_act == "none":
+                raise ValueError("s_activation='none' has no hidden activation to apply; "
+                                 "use 'relu' or 'tanh'")
             return LegacyRealNvpFlow(dim, layers=layers, hidden_size=hidden, activation=act,
-                                     s_activation=s_activation or "relu")
+                                     s_activation=s_act)
         return super().__new__(cls)
 
     def __init__(self, dim, *args, mask_mode="flip_data", s_activation=None, **kwargs):

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define CNF_ABI_VERSION 1
+#define CNF_ABI_VERSION 2   /* 2: cnf_adam_step takes double hyper-parameters */
 #define CNF_MAX_HIDDEN 8    /* hidden layers per conditioner MLP            */
 #define CNF_MAX_DIM 256     /* logit-vector width D                         */
 #define CNF_MAX_WIDTH 512   /* any MLP width                                */
@@ -173,11 +173,6 @@ int cnf_loss_vjp(const cnf_desc* desc, const void* prepared, const float* x,
                  float* loss_terms, float* grads, float* dx, int64_t B, void* workspace,
                  size_t workspace_bytes, void* stream);
 
-/* Which kernel family serves this descriptor's launches: "sgpr-fused"
- * (pipelined scalar weights, every output mode), "valu-fused" (strict_nan,
- * shapes whose Linears exceed 32 floats, misaligned views), "mfma-wide"
- * (register-resident MFMA, the wide shapes of its table), "mfma-tile" (other
- * wide shapes, every-layer outputs of wide stacks). */
 /* Reverse mode of cnf_inverse (autograd through Flow.backward, flows/flows.py:
  * 27-37 / 114-126): given upstream gradients of the inverse's outputs, writes
  *   grads  [cnf_param_count]  d/d(parameters), state_dict order (overwritten)
@@ -199,11 +194,20 @@ int cnf_vjp_inverse(const cnf_desc* desc, const void* prepared, const float* z, 
  *               in place (the tensors cnf_prepare reads)
  *   grads       [cnf_param_count]  flat, state_dict order
  *   exp_avg, exp_avg_sq  [cnf_param_count] moments, zero before step 1
- *   step        1-based step count (bias corrections) */
+ *   step        1-based step count (bias corrections)
+ *   lr, beta1, beta2, eps, weight_decay   as the torch optimizer holds them
+ *               (Python floats = doubles): 1 - beta, the bias corrections and
+ *               lr / (1 - beta1^t) are formed in double and rounded to fp32
+ *               once, as torch's scalar arguments are */
 int cnf_adam_step(const cnf_desc* desc, float* const* params, const float* grads,
-                  float* exp_avg, float* exp_avg_sq, int64_t step, float lr, float beta1,
-                  float beta2, float eps, float weight_decay, void* stream);
+                  float* exp_avg, float* exp_avg_sq, int64_t step, double lr, double beta1,
+                  double beta2, double eps, double weight_decay, void* stream);
 
+/* Which kernel family serves this descriptor's launches: "sgpr-fused"
+ * (pipelined scalar weights, every output mode), "valu-fused" (strict_nan,
+ * shapes whose Linears exceed 32 floats, misaligned views), "mfma-wide"
+ * (register-resident MFMA, the wide shapes of its table), "mfma-tile" (other
+ * wide shapes, every-layer outputs of wide stacks). */
 const char* cnf_kernel_name(const cnf_desc* desc);
 
 const char* cnf_strerror(int status);

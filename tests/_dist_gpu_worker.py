@@ -1,7 +1,9 @@
-"""One rank of tests/test_gpu_dist.py: the data-parallel trainer on cuda:0
-with the gloo backend on device tensors (two ranks share the one GPU of the
-test box; RCCL refuses two ranks per device).  Runs the native fused
-loss + VJP kernels (cnf_loss_vjp) and the fused eval (cnf_forward_loss)."""
+"""One rank of tests/test_gpu_dist.py: the data-parallel trainer on device
+tensors.  Backend "gloo" (argv[2], the default): every rank on cuda:0 (two
+ranks share the one GPU of the test box; RCCL refuses two ranks per device).
+Backend "nccl" (RCCL over xGMI): rank r on cuda:LOCAL_RANK, one GPU each.
+Runs the native fused loss + VJP kernels (cnf_loss_vjp), the native Adam step
+(cnf_adam_step) and the fused eval (cnf_forward_loss)."""
 import os
 import sys
 
@@ -40,10 +42,14 @@ def data(dev):
 
 def main():
     out = sys.argv[1]
+    backend = sys.argv[2] if len(sys.argv) > 2 else "gloo"
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
-    dev = torch.device("cuda", 0)
+    dev = torch.device("cuda", int(os.environ["LOCAL_RANK"]) if backend == "nccl" else 0)
     torch.cuda.set_device(dev)
-    dist.init_process_group("gloo", init_method="env://")
+    if backend == "nccl":
+        dist.init_process_group("nccl", init_method="env://", device_id=dev)
+    else:
+        dist.init_process_group("gloo", init_method="env://")
     from cnf_hip import engine
     from cnf_hip.dist import ShardedFlowTrainer, shard
     f = make_flow()
@@ -56,14 +62,15 @@ def main():
     x, y = data(dev)
     a, b = shard(N, rank, world)
     n0 = engine.stats["loss_vjp"]
+    a0 = engine.stats.get("adam", 0)
     terms = [tr.step(x[a:b], y[a:b], N) for _ in range(STEPS)]
     ev = tr.evaluate(x[a:b], y[a:b])
-    native = engine.stats["loss_vjp"] - n0
+    native = min(engine.stats["loss_vjp"] - n0, engine.stats.get("adam", 0) - a0)
     torch.cuda.synchronize()
     if rank == 0:
         torch.save({"params": {k: v.detach().cpu().clone() for k, v in f.state_dict().items()},
                     "terms": torch.stack(terms).cpu(), "eval": ev.cpu(),
-                    "native_steps": native}, out)
+                    "native_steps": native, "world": world, "backend": backend}, out)
     dist.barrier()
     dist.destroy_process_group()
 

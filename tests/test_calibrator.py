@@ -13,18 +13,22 @@ from flows.nice_torch import NiceFlow
 import calibrators as C
 
 
-def _g7():
-    f = np.load(os.path.join(GOLDEN, "g7_calibrator_d3.npz"))
+def _g7(name="g7_calibrator_d3"):
+    f = np.load(os.path.join(GOLDEN, name + ".npz"))
     return json.loads(str(f["meta"])), f
 
 
-def _fit(dev):
-    meta, f = _g7()
+G7B = "g7b_calibrator_d3_mb128"  # batch_size=128: the DataLoader order is pinned too
+
+
+def _fit(dev, name="g7_calibrator_d3"):
+    meta, f = _g7(name)
     torch.manual_seed(meta["seed"])
     np.random.seed(meta["seed"])
+    kw = {"batch_size": meta["batch_size"]} if "batch_size" in meta else {}
     return C.TorchFlowCalibrator(RealNvpFlow, f["x"].astype(np.float64), f["y"], layers=5,
                                  hidden_size=[3, 3], epochs=meta["epochs"],
-                                 dev=torch.device(dev)), f
+                                 dev=torch.device(dev), **kw), f
 
 
 def _check(cal, f, tol):
@@ -55,6 +59,46 @@ def test_calibrator_native_matches_reference():
     assert cal.history["loss"][0].device.type == "cuda"     # no host sync per epoch
     assert next(cal.flow.parameters()).device.type == "cpu"  # flow returned to host
     _check(cal, f, 1e-5)
+
+
+def test_calibrator_minibatch_cpu_matches_reference():
+    """g7b: the reference's own minibatch fit (batch_size=128 of N=600)."""
+    cal, f = _fit("cpu", G7B)
+    _check(cal, f, 1e-5)
+
+
+@pytest.mark.gpu
+def test_calibrator_native_minibatch_matches_reference():
+    """The native fit draws each pass's order as DataLoader(shuffle=True)
+    does (calibrators._loader_order), so its 5 batches per epoch, weights,
+    history (the last eval batch's sums) and predictions match g7b."""
+    from cnf_hip import engine
+    n0 = engine.stats["loss_vjp"]
+    cal, f = _fit("cuda:0", G7B)
+    meta, _ = _g7(G7B)
+    assert engine.stats["loss_vjp"] >= n0 + meta["epochs"] * 5, "fused native step did not run"
+    _check(cal, f, 1e-5)
+    # the torch optimizer received the native Adam's state
+    st = cal.optimizer.state[cal.flow.layers[0].s.layers[0].weight]
+    assert int(st["step"]) == meta["epochs"] * 5
+
+
+@pytest.mark.parametrize("n,bs", [(600, 128), (7, 3), (5, 5), (1, 4)])
+def test_loader_order_is_the_dataloader_order(n, bs):
+    """calibrators._loader_order reproduces DataLoader(TensorDataset, bs,
+    shuffle=True)'s batches AND leaves torch's global CPU RNG where the loader
+    leaves it (two passes in a row)."""
+    from torch.utils.data import DataLoader, TensorDataset
+    dl = DataLoader(TensorDataset(torch.arange(n)), batch_size=bs, shuffle=True)
+    torch.manual_seed(11)
+    ref = [torch.cat([b[0] for b in dl]) for _ in range(2)]
+    after_ref = torch.rand(3)
+    torch.manual_seed(11)
+    got = [C._loader_order(n) for _ in range(2)]
+    after_got = torch.rand(3)
+    for a, b in zip(got, ref):
+        assert torch.equal(a, b)
+    assert torch.equal(after_got, after_ref)
 
 
 def test_calibrator_nice_factory_and_minibatches_cpu():

@@ -1,10 +1,11 @@
-"""The data-parallel composition on the GPU: two ranks (processes) each run
-the native fused loss + VJP kernels on their shard and add gradients with one
-all-reduce per step (cnf_hip/dist.py).  The result must equal single-process
-full-batch training on the same kernels and the reference's loss
-(calibrators.py:284-295) at <= 1e-5.  gloo on device tensors: both ranks share
-the test box's one GPU, which RCCL does not allow; the bench's multi-GPU runs
-use RCCL."""
+"""The data-parallel composition on the GPU: ranks (processes) each run the
+native fused loss + VJP kernels on their shard, add gradients with one
+all-reduce per step and step Adam natively (cnf_hip/dist.py).  The result must
+equal single-process full-batch training and the reference's loss
+(calibrators.py:284-295) at <= 1e-5.
+  * gloo, 2 ranks on one device (always runs: RCCL refuses two ranks per GPU);
+  * nccl (RCCL over xGMI), one rank per visible GPU (configs[2]'s collective),
+    skipped on a box with fewer than 2 GPUs."""
 import os
 import socket
 import subprocess
@@ -27,17 +28,21 @@ def _free_port():
     return port
 
 
-def test_two_rank_native_sharded_training_equals_full_batch():
+def _visible_gpus():
+    # device_count() does not initialise the GPU in this (parent) process
+    return torch.cuda.device_count()
+
+
+def _run_ranks(world, backend):
     import _dist_gpu_worker as W
-    from cnf_hip import vjp as V
     out = os.path.join(tempfile.mkdtemp(), "r0.pt")
     port = str(_free_port())
     procs = []
-    for r in range(2):
-        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r),
+                   LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "_dist_gpu_worker.py"),
-                                       out], env=env))
+                                       out, backend], env=env))
     codes = []
     for p in procs:
         try:
@@ -45,10 +50,29 @@ def test_two_rank_native_sharded_training_equals_full_batch():
         except subprocess.TimeoutExpired:
             p.kill()
             codes.append(-9)
-    assert codes == [0, 0], codes
+    assert codes == [0] * world, codes
     got = torch.load(out, weights_only=True)
-    assert got["native_steps"] == W.STEPS, "ranks did not run the native cnf_loss_vjp"
+    assert got["native_steps"] == W.STEPS, "ranks did not run cnf_loss_vjp + cnf_adam_step"
+    assert got["world"] == world and got["backend"] == backend
+    _check_against_full_batch(got)
 
+
+def test_two_rank_native_sharded_training_equals_full_batch():
+    _run_ranks(2, "gloo")
+
+
+def test_rccl_all_gpus_sharded_training_equals_full_batch():
+    """The RCCL path of configs[2]: one rank per visible GPU (at most 8),
+    backend nccl (= RCCL over xGMI on ROCm).  Needs a multi-GPU box."""
+    n = min(_visible_gpus(), 8)
+    if n < 2:
+        pytest.skip("needs >= 2 visible GPUs for an RCCL run (%d visible)" % n)
+    _run_ranks(n, "nccl")
+
+
+def _check_against_full_batch(got):
+    import _dist_gpu_worker as W
+    from cnf_hip import vjp as V
     # single process, full batch, the same native kernels
     f = W.make_flow().to(DEV)
     stack = f._native_stack()

@@ -1,0 +1,41 @@
+#!/bin/bash
+# Named GPU steps for one gpurun call, each under its own time limit; the first
+# step that faults, aborts or times out ends the script (exit codes other than
+# 0 / 1, which only mean "tests failed").  Logs: gpurun_out/<step>.log.
+# Usage: bash tools/gpu_steps.sh step [step ...]
+#   tests        pytest -m gpu (whole GPU suite)
+#   smoke        __graft_entry__.smoke()
+#   bench        python bench.py (default line)
+#   trace        k_sgpr per-wave timeline (libcnf_hip_trace.so), loss + forward
+#   rate         tools/quick_rate.py loss / forward (2^20 and 2^23 rows)
+#   ab           tools/quick_rate.py loss for every gpurun_out/../tools/ab/lib*.so
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+run() {
+  local name=$1; shift
+  local t0=$(date +%s)
+  timeout -k 10 "$@" > gpurun_out/$name.log 2>&1
+  local rc=$?
+  echo "$name rc=$rc ($(( $(date +%s) - t0 ))s)"
+  tail -n ${TAILN:-4} gpurun_out/$name.log | grep -v amdgpu.ids
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+}
+for step in "$@"; do
+  case "$step" in
+    tests) TAILN=12 run tests 600 python -u -m pytest tests -m gpu -q -rfs --timeout 120 --timeout-method thread ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) TAILN=2 run bench 600 python bench.py ;;
+    trace) run trace_loss 180 python tools/sgpr_trace.py loss && run trace_fwd 180 python tools/sgpr_trace.py forward ;;
+    rate) run rate_loss 300 python tools/quick_rate.py loss && run rate_fwd 300 python tools/quick_rate.py forward ;;
+    ab)
+      for lib in tools/ab/lib*.so; do
+        [ -e "$lib" ] || continue
+        n=$(basename "$lib" .so)
+        CNF_HIP_LIB=$PWD/$lib run "ab_$n" 300 python tools/quick_rate.py ${AB_MODE:-loss}
+      done ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+exit 0
