@@ -109,6 +109,82 @@ def _loader_order(n):
     return order.pin_memory() if torch.cuda.is_available() else order
 
 
+class _EpochRunner:
+    """One training epoch of TorchFlowCalibrator.fit on the fused kernels
+    (calibrators.py:284-317): gather the pass's rows in loader order, per
+    batch cnf_loss_vjp + Adam, then the eval pass's cnf_forward_loss per batch,
+    whose LAST batch's sums are the epoch's history terms."""
+
+    def __init__(self, stack, adam, logits, target, bs):
+        self.stack, self.adam, self.x, self.y, self.bs = stack, adam, logits, target, bs
+        self.N = logits.shape[0]
+        self.nb = (self.N + bs - 1) // bs
+
+    def body(self, order_tr, order_ev, terms_out, sched=None):
+        from cnf_hip import vjp as V
+        N, bs = self.N, self.bs
+        xs, ys = self.x.index_select(0, order_tr), self.y.index_select(0, order_tr)
+        for b, s in enumerate(range(0, N, bs)):
+            xb, yb = xs[s:s + bs], ys[s:s + bs]
+            _, grads, _ = V.loss_and_grads(self.stack, xb, yb, grad_scale=1.0 / xb.shape[0])
+            if sched is None:
+                self.adam.step(grads)
+            else:
+                self.adam.step_sched(grads, sched[b])
+        xe, ye = self.x.index_select(0, order_ev), self.y.index_select(0, order_ev)
+        for s in range(0, N, bs):
+            last = s + bs >= N
+            self.stack.forward_loss(xe[s:s + bs], ye[s:s + bs],
+                                    terms_out=terms_out if last else None)
+
+    def eager_epoch(self, terms_out):
+        dev = self.x.device
+        o_tr = _loader_order(self.N).to(dev, non_blocking=True)
+        o_ev = _loader_order(self.N).to(dev, non_blocking=True)
+        self.body(o_tr, o_ev, terms_out)
+
+
+class _EpochGraph:
+    """K epochs of _EpochRunner captured once as a HIP graph (torch.cuda.graph;
+    every launch of the C ABI goes to the capturing stream).  Per replay the
+    host draws the K epochs' loader orders (the global CPU RNG advances as the
+    reference's DataLoader would) and the Adam scalars of the K * nb steps,
+    stages both with ONE host-to-device copy into the graph's static buffers,
+    replays, and copies the K per-epoch terms out."""
+
+    CHUNK = 50
+
+    def __init__(self, run, K):
+        self.run, self.K = run, K
+        N, nb, dev = run.N, run.nb, run.x.device
+        self.ord = torch.empty(K, 2, N, dtype=torch.int64, device=dev)
+        self.sched = torch.empty(K, nb, 2, dtype=torch.float32, device=dev)
+        self.terms = torch.empty(K, 3, dtype=torch.float32, device=dev)
+        run.stack.invalidate()  # the graph's first launch re-prepares the weights
+        t0 = run.adam.t
+        torch.cuda.synchronize(dev)
+        self.g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.g):
+            for k in range(K):
+                run.body(self.ord[k, 0], self.ord[k, 1], self.terms[k], sched=self.sched[k])
+        run.adam.t = t0  # capture recorded the steps; replays perform them
+
+    def replay(self, terms_dst):
+        run, K, N, nb = self.run, self.K, self.run.N, self.run.nb
+        orders = torch.empty(K, 2, N, dtype=torch.int64)
+        for k in range(K):
+            orders[k, 0] = _loader_order(N)
+            orders[k, 1] = _loader_order(N)
+        t = run.adam.t
+        sched = torch.tensor([run.adam.sched_values(t + 1 + i) for i in range(K * nb)],
+                             dtype=torch.float32).reshape(K, nb, 2)
+        self.ord.copy_(orders.pin_memory(), non_blocking=True)
+        self.sched.copy_(sched.pin_memory(), non_blocking=True)
+        self.g.replay()
+        run.adam.t = t + K * nb
+        terms_dst.copy_(self.terms)
+
+
 class TorchFlowCalibrator(Calibrator):
     """Trains a normalizing flow on (logits, target) by minimising
     -mean(log(softmax(f(x))[y] + 1e-7) + log|det J_f(x)|)  (calibrators.py:239-353)."""
@@ -125,6 +201,8 @@ class TorchFlowCalibrator(Calibrator):
         self.optimizer = torch.optim.Adam(self.flow.parameters())
         self._replica = None
         self._lp_dev = None
+        # native fit: replay chunks of epochs as HIP graphs (False: eager epochs)
+        self._graph_ok = bool(kwargs.get('cnf_graph', True))
         self.history = self.fit(self.logits, self.target,
                                 epochs=kwargs.get('epochs', 1000),
                                 batch_size=kwargs.get('batch_size', logits.shape[0]))
@@ -185,39 +263,36 @@ class TorchFlowCalibrator(Calibrator):
         evaluation batch.  Each pass over the data draws its order exactly as
         the reference's DataLoader(shuffle=True) does (_loader_order), so
         minibatch runs see the reference's batches and the eval history keeps
-        the reference's last-batch value (calibrators.py:274-317)."""
-        from cnf_hip import vjp as V
+        the reference's last-batch value (calibrators.py:274-317).
+
+        After one eager epoch, chunks of epochs run as ONE captured HIP graph
+        each (_EpochGraph): the chunk's orders and Adam step scalars are staged
+        with one host-to-device copy, so the host issues three operations per
+        chunk instead of ~10 launches per epoch.  kwargs cnf_graph=False keeps
+        every epoch eager."""
         from cnf_hip.adam import StackAdam
-        # the optimizer step on the device in one launch, with the torch Adam's
-        # current hyper-parameters and state (written back after the fit)
         adam = StackAdam.like(stack, self.optimizer)
         N = logits.shape[0]
         bs = max(1, int(batch_size))
-        history = {'loss': [], 'ce': [], 'log_det': []}
-        dev = logits.device
-
-        def batches():
-            # one gather of the permuted rows per pass; batches are views
-            order = _loader_order(N).to(dev, non_blocking=True)
-            xs, ys = logits.index_select(0, order), target.index_select(0, order)
-            return [(xs[s:s + bs], ys[s:s + bs]) for s in range(0, N, bs)]
-
-        for epoch in range(epochs):
-            self.flow.train()
-            for xb, yb in batches():
-                _, grads, _ = V.loss_and_grads(stack, xb, yb, grad_scale=1.0 / xb.shape[0])
-                adam.step(grads)
-            self.flow.eval()
-            num = 0
-            terms = None
-            for xb, yb in batches():
-                terms, _, _ = stack.forward_loss(xb, yb)
-                num += xb.shape[0]
-            history['loss'].append(terms[0] / num)
-            history['ce'].append(terms[1] / num)
-            history['log_det'].append(terms[2] / num)
+        terms_all = torch.empty(max(epochs, 1), 3, dtype=torch.float32, device=logits.device)
+        run = _EpochRunner(stack, adam, logits, target, bs)
+        e = 0
+        if epochs > 0:  # the eager first epoch also builds every cached buffer
+            run.eager_epoch(terms_all[0])
+            e = 1
+        if self._graph_ok and epochs - e >= 2:
+            g = _EpochGraph(run, min(epochs - e, _EpochGraph.CHUNK))
+            while epochs - e >= g.K:
+                g.replay(terms_all[e:e + g.K])
+                e += g.K
+        while e < epochs:
+            run.eager_epoch(terms_all[e])
+            e += 1
         adam.store_into(self.optimizer)
-        return history
+        stack.invalidate()  # drop blobs / workspaces captured into a graph pool
+        hist = terms_all[:epochs] / N
+        return {'loss': list(hist[:, 0].unbind(0)), 'ce': list(hist[:, 1].unbind(0)),
+                'log_det': list(hist[:, 2].unbind(0))}
 
     # -------------------------------------------------------------- predict
     def _device_flow(self):

@@ -69,7 +69,15 @@ class StackAdam:
             }
             off += n
 
-    def step(self, flat_grads):
+    def sched_values(self, t):
+        """torch.optim.Adam's two step-dependent scalars for step t, formed as
+        torch forms them (Python doubles, torch/optim/adam.py
+        _single_tensor_adam), for cnf_adam_step_sched: [lr / (1 - beta1^t),
+        (1 - beta2^t) ** 0.5]."""
+        b1, b2 = self.betas
+        return (self.lr / (1 - b1 ** t), (1 - b2 ** t) ** 0.5)
+
+    def _ensure_state(self):
         ps = self.stack.param_tensors()
         dev = ps[0].device
         if self._m is None:
@@ -78,6 +86,25 @@ class StackAdam:
             self._v = torch.zeros(n, dtype=torch.float32, device=dev)
         elif self._m.device != dev:
             self._m, self._v = self._m.to(dev), self._v.to(dev)
+        return ps, dev
+
+    def step_sched(self, flat_grads, sched):
+        """One step whose scalars come from the device tensor `sched` [2]
+        (graph capture: replays any step).  Advances the host step count."""
+        ps, dev = self._ensure_state()
+        self.t += 1
+        arr = (ctypes.c_void_p * len(ps))(*[p.data_ptr() for p in ps])
+        st = _lib.lib().cnf_adam_step_sched(
+            ctypes.byref(self.stack.desc), arr, _ptr(flat_grads), _ptr(self._m), _ptr(self._v),
+            _ptr(sched), ctypes.c_double(self.betas[0]), ctypes.c_double(self.betas[1]),
+            ctypes.c_double(self.eps), ctypes.c_double(self.weight_decay), _stream(dev))
+        _lib.check("cnf_adam_step_sched", st)
+        for p in ps:
+            torch.autograd.graph.increment_version(p)
+        stats["adam"] = stats.get("adam", 0) + 1
+
+    def step(self, flat_grads):
+        ps, dev = self._ensure_state()
         for p in ps:
             if not p.is_contiguous():
                 raise ValueError("StackAdam needs contiguous parameters")

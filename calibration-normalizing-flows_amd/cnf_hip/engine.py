@@ -222,10 +222,12 @@ class CouplingStack:
             fin = allt[-1]
         return fin, ld, allt
 
-    def forward_loss(self, x, y, kind=_lib.LOSS_CAL, det=1.0, want_outputs=False):
+    def forward_loss(self, x, y, kind=_lib.LOSS_CAL, det=1.0, want_outputs=False,
+                     terms_out=None):
         """Fused forward + log-det + loss terms (cnf_forward_loss): returns
         (terms[3] = sums over the rows of (loss, ce, log-det), z or None, ld or None).
-        A label outside [0, D) makes the terms NaN (the reference raises)."""
+        A label outside [0, D) makes the terms NaN (the reference raises).
+        terms_out: a caller-provided fp32 [3] destination on x's device."""
         x = self._check_input(x)
         y = y.contiguous().to(torch.int64)
         B = x.shape[0]
@@ -243,7 +245,9 @@ class CouplingStack:
         if ws is None or ws.numel() < n.value:
             ws = torch.zeros(max(n.value, 16), dtype=torch.uint8, device=dev)
             self._loss_ws[sk] = ws
-        terms = torch.empty(3, dtype=torch.float32, device=dev)
+        terms = torch.empty(3, dtype=torch.float32, device=dev) if terms_out is None else terms_out
+        if terms.numel() != 3 or terms.dtype != torch.float32 or terms.device != dev:
+            raise ValueError("forward_loss: terms_out must be fp32 [3] on %s" % dev)
         z = torch.empty_like(x) if want_outputs else None
         ld = torch.empty(B, dtype=torch.float32, device=dev) if want_outputs else None
         st = lib.cnf_forward_loss(ctypes.byref(self.desc), _ptr(blob), _ptr(x), _ptr(y),

@@ -32,12 +32,17 @@ struct AdamArgs {
   // formed in double from the optimizer's Python floats (torch/optim/adam.py
   // _single_tensor_adam: lerp_(grad, 1 - beta1), addcmul_(value=1 - beta2))
   float omb1, beta2, omb2, eps, wd, step_size, bc2_sqrt;
+  // device {step_size, bc2_sqrt} (cnf_adam_step_sched: graph-captured steps,
+  // whose kernel arguments are fixed at capture); nullptr: the two above
+  const float* sched;
 };
 
 __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
   const int ti = blockIdx.y;
   const int64_t o0 = a.off[ti], n = a.off[ti + 1] - o0;
   float* __restrict__ p = a.p[ti];
+  const float step_size = a.sched ? a.sched[0] : a.step_size;
+  const float bc2_sqrt = a.sched ? a.sched[1] : a.bc2_sqrt;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     const int64_t f = o0 + i;
     const float pv = p[i];
@@ -50,8 +55,8 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
                               __fmul_rn(__fmul_rn(g, g), a.omb2));         // mul_().addcmul_()
     a.m[f] = m;
     a.v[f] = v;
-    const float denom = __fadd_rn(__fdiv_rn(sqrtf(v), a.bc2_sqrt), a.eps);
-    p[i] = __fadd_rn(pv, __fmul_rn(-a.step_size, __fdiv_rn(m, denom)));  // addcdiv_
+    const float denom = __fadd_rn(__fdiv_rn(sqrtf(v), bc2_sqrt), a.eps);
+    p[i] = __fadd_rn(pv, __fmul_rn(-step_size, __fdiv_rn(m, denom)));    // addcdiv_
   }
 }
 
@@ -60,20 +65,22 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
 
 using namespace cnf;
 
-extern "C" int cnf_adam_step(const cnf_desc* desc, float* const* params, const float* grads,
-                             float* exp_avg, float* exp_avg_sq, int64_t step, double lr,
-                             double beta1, double beta2, double eps, double weight_decay,
-                             void* stream) {
+namespace {
+
+int adam_launch(const cnf_desc* desc, float* const* params, const float* grads, float* exp_avg,
+                float* exp_avg_sq, int64_t step, double lr, double beta1, double beta2, double eps,
+                double weight_decay, const float* sched, void* stream) {
   Shape s;
   int st = derive_shape(desc, &s);
   if (st != CNF_OK) return st;
-  if (step < 1) return CNF_ERR_DESC;
+  if (!sched && step < 1) return CNF_ERR_DESC;
   const int nt = s.L * s.nets * s.n_lin * 2;
   if (nt == 0) return CNF_OK;
   if (!params || !grads || !exp_avg || !exp_avg_sq) return CNF_ERR_NULL;
-  const double bc1 = 1.0 - std::pow(beta1, (double)step);
-  const double bc2 = 1.0 - std::pow(beta2, (double)step);
+  const double bc1 = sched ? 1.0 : 1.0 - std::pow(beta1, (double)step);
+  const double bc2 = sched ? 1.0 : 1.0 - std::pow(beta2, (double)step);
   AdamArgs a{};
+  a.sched = sched;
   a.g = grads;
   a.m = exp_avg;
   a.v = exp_avg_sq;
@@ -121,4 +128,23 @@ extern "C" int cnf_adam_step(const cnf_desc* desc, float* const* params, const f
     return CNF_ERR_HIP;
   }
   return CNF_OK;
+}
+
+}  // namespace
+
+extern "C" int cnf_adam_step(const cnf_desc* desc, float* const* params, const float* grads,
+                             float* exp_avg, float* exp_avg_sq, int64_t step, double lr,
+                             double beta1, double beta2, double eps, double weight_decay,
+                             void* stream) {
+  return adam_launch(desc, params, grads, exp_avg, exp_avg_sq, step, lr, beta1, beta2, eps,
+                     weight_decay, nullptr, stream);
+}
+
+extern "C" int cnf_adam_step_sched(const cnf_desc* desc, float* const* params,
+                                   const float* grads, float* exp_avg, float* exp_avg_sq,
+                                   const float* sched, double beta1, double beta2, double eps,
+                                   double weight_decay, void* stream) {
+  if (!sched) return CNF_ERR_NULL;
+  return adam_launch(desc, params, grads, exp_avg, exp_avg_sq, 0, 0.0, beta1, beta2, eps,
+                     weight_decay, sched, stream);
 }

@@ -203,6 +203,14 @@ int cnf_adam_step(const cnf_desc* desc, float* const* params, const float* grads
                   float* exp_avg, float* exp_avg_sq, int64_t step, double lr, double beta1,
                   double beta2, double eps, double weight_decay, void* stream);
 
+/* The same step with its two step-dependent scalars read from DEVICE memory,
+ * so a HIP graph captured once replays any step (kernel arguments are fixed at
+ * capture):  sched[0] = (float)(lr / (1 - beta1^t)),
+ *            sched[1] = (float)sqrt(1 - beta2^t)   (formed in double). */
+int cnf_adam_step_sched(const cnf_desc* desc, float* const* params, const float* grads,
+                        float* exp_avg, float* exp_avg_sq, const float* sched, double beta1,
+                        double beta2, double eps, double weight_decay, void* stream);
+
 /* Which kernel family serves this descriptor's launches: "sgpr-fused"
  * (pipelined scalar weights, every output mode), "valu-fused" (strict_nan,
  * shapes whose Linears exceed 32 floats, misaligned views), "mfma-wide"
