@@ -62,6 +62,13 @@
 // (100 MHz) marks [start, tile0 data, tile0 done, tile1 data, tile1 done,
 // last tile done, end, hw id] of the last launch, read by tools/sgpr_trace.py.
 __device__ unsigned long long cnf_trace[16384 * 8];
+// shader-clock stamps (s_memtime) at the wave's start and end: the in-kernel
+// clock is their difference over the s_memrealtime (100 MHz) difference
+__device__ unsigned long long cnf_trace_clk[16384 * 2];
+#define CNF_TRC(slot)                                                                   \
+  do {                                                                                  \
+    if (lane == 0 && gw < 16384) cnf_trace_clk[gw * 2 + (slot)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
 #define CNF_TR(slot)                                                                   \
   do {                                                                                 \
     if (lane == 0 && gw < 16384) cnf_trace[gw * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
@@ -69,6 +76,9 @@ __device__ unsigned long long cnf_trace[16384 * 8];
 #else
 #define CNF_TR(slot) \
   do {               \
+  } while (0)
+#define CNF_TRC(slot) \
+  do {                \
   } while (0)
 #endif
 
@@ -78,6 +88,19 @@ namespace {
 using namespace valu;
 
 constexpr int kWaves = 4;  // waves per block
+
+// Output path of the full tiles (cnf_sgpr_common.h stage_pairs / store_tile):
+//   0  16-B stores straight from registers, deferred one tile (round 2);
+//   1  staged through the wave's LDS tile, stored lane-linear; the next
+//      tile's LDS-DMA is issued after the staged tile has been read back;
+//   2  staged through a second LDS tile per wave, stores deferred one tile,
+//      the next tile's DMA issued before the compute (twice the LDS).
+#ifndef CNF_SGPR_STAGE
+#define CNF_SGPR_STAGE 1
+#endif
+constexpr int kStage = CNF_SGPR_STAGE;
+
+
 
 // Row pairs per lane.  Two pairs (4 rows per lane) let each SGPR weight feed
 // two FMAs (half the scalar-load traffic per row), at 4 waves per SIMD instead
@@ -95,10 +118,12 @@ constexpr int pairs_per_lane() { return (ALL || PERM) ? 1 : CNF_SGPR_PAIRS; }
 #endif
 template <int MODE, bool ALL, bool PERM>
 constexpr int waves_per_simd() {
-  return pairs_per_lane<ALL, PERM>() == 2 ? 4 : (PERM ? 4 : CNF_SGPR_WPS);
+  return pairs_per_lane<ALL, PERM>() == 2 ? 4 : (PERM || kStage == 2 ? 4 : CNF_SGPR_WPS);
 }
 
 enum Mode { kFwd = 0, kInv = 1, kLoss = 2, kPredict = 3 };
+
+
 
 // Conditioner activations of the lane's P row pairs (pair-major).
 template <int D, int H1, int H2, int P>
@@ -135,8 +160,13 @@ __device__ __forceinline__ void slin(const SW<NC>& w, X&& x, E&& emit, F&& befor
     for (int o = 0; o < NOUT; ++o)
 #pragma unroll
       for (int q = 0; q < P; ++q) {
+#ifdef CNF_AB_FMA_BUILTIN  // A/B: the compiler's broadcast (copies odd weights to a scratch pair)
         if (RELU && k == NIN - 1) a[o][q] = fma_clamp(w[o * S + 1 + k], x(q, k), a[o][q]);
         else a[o][q] = fmaT(w[o * S + 1 + k], x(q, k), a[o][q]);
+#else
+        if (RELU && k == NIN - 1) a[o][q] = fma_ws_clamp(w, o * S + 1 + k, x(q, k), a[o][q]);
+        else a[o][q] = fma_ws(w, o * S + 1 + k, x(q, k), a[o][q]);
+#endif
       }
 #pragma unroll
   for (int o = 0; o < NOUT; ++o) emit(o, a[o]);
@@ -463,6 +493,7 @@ __global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) v
 
   // -------- full tiles: LDS-DMA in, deferred 16-B stores out --------
   CNF_TR(0);
+  CNF_TRC(0);
 #ifdef CNF_SGPR_TRACE
   if (lane == 0 && gw < 16384)
     cnf_trace[gw * 8 + 7] = ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
@@ -471,14 +502,17 @@ __global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) v
 #endif
   int t = gw;
   if (t < nfull) wave_dma<D, TR>(sm, a.in + (int64_t)t * TF, lane);
-  f2 pz[P][D], pld[P];
+  [[maybe_unused]] float* stg = smem + (kWaves + wv) * TF;  // kStage 2: the output tile
+  f2 pz[kStage == 0 ? P : 1][D], pld[P];
   int64_t prow = -1;  // first row of the lane's pending (not yet stored) outputs
   for (; t < nfull; t += nw) {
     --left;  // tiles after this one
+#ifndef CNF_AB_NO_PRIO
     if (left >= 3) __builtin_amdgcn_s_setprio(3);
     else if (left == 2) __builtin_amdgcn_s_setprio(2);
     else if (left == 1) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(0);
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA has landed
     f2 v[P][D];
     read_pairs<D, P>(sm, lane, v);
@@ -487,11 +521,15 @@ __global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) v
     if (ntr < 2) CNF_TR(1 + 2 * ntr);
 #endif
     const int64_t row0 = (int64_t)t * TR;
-    if (prow >= 0) {  // the previous tile's outputs, issued after this tile's reads
-      if (a.out) store_rows<D, P>(a.out + prow * D, pz, 2 * P, al);
+    if (kStage != 1 && prow >= 0) {  // the previous tile's outputs, after this tile's reads
+      if constexpr (kStage == 0) {
+        if (a.out) store_rows<D, P>(a.out + prow * D, pz, 2 * P, al);
+      } else {
+        if (a.out) store_tile<TF>(a.out + (prow - 2 * P * lane) * D, stg, lane);
+      }
       if (a.ld) store_lds<P>(a.ld + prow, pld, 2 * P, al_ld);
     }
-    if (t + nw < nfull) wave_dma<D, TR>(sm, a.in + (int64_t)(t + nw) * TF, lane);
+    if (kStage != 1 && t + nw < nfull) wave_dma<D, TR>(sm, a.in + (int64_t)(t + nw) * TF, lane);
     uint32_t lab = 0;
     if constexpr (MODE == kLoss) lab = load_labels<D, P>(a.y + row0 + 2 * P * lane, 2 * P, y16);
     f2 ld[P];
@@ -502,16 +540,36 @@ __global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) v
     CNF_TR(5);
     ++ntr;
 #endif
+    if constexpr (kStage == 1) {
+      // stage in the input tile (its rows are in registers), store lane-linear,
+      // then let the next tile's DMA in once the staged reads have completed
+      if (a.out) {
+        stage_pairs<D, P>(sm, lane, v);
+        store_tile<TF>(a.out + row0 * D, sm, lane);
+      }
+      if (a.ld) store_lds<P>(a.ld + row0 + 2 * P * lane, ld, 2 * P, al_ld);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (t + nw < nfull) wave_dma<D, TR>(sm, a.in + (int64_t)(t + nw) * TF, lane);
+    } else {
+      if constexpr (kStage == 0) {
 #pragma unroll
-    for (int p = 0; p < P; ++p) {
+        for (int p = 0; p < P; ++p)
 #pragma unroll
-      for (int k = 0; k < D; ++k) pz[p][k] = v[p][k];
-      pld[p] = ld[p];
+          for (int k = 0; k < D; ++k) pz[p][k] = v[p][k];
+      } else {
+        if (a.out) stage_pairs<D, P>(stg, lane, v);
+      }
+#pragma unroll
+      for (int p = 0; p < P; ++p) pld[p] = ld[p];
+      prow = row0 + 2 * P * lane;
     }
-    prow = row0 + 2 * P * lane;
   }
-  if (prow >= 0) {
-    if (a.out) store_rows<D, P>(a.out + prow * D, pz, 2 * P, al);
+  if (kStage != 1 && prow >= 0) {
+    if constexpr (kStage == 0) {
+      if (a.out) store_rows<D, P>(a.out + prow * D, pz, 2 * P, al);
+    } else {
+      if (a.out) store_tile<TF>(a.out + (prow - 2 * P * lane) * D, stg, lane);
+    }
     if (a.ld) store_lds<P>(a.ld + prow, pld, 2 * P, al_ld);
   }
   // -------- the ragged last tile (B % TR rows): plain loads, masked stores --------
@@ -536,8 +594,11 @@ __global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) v
     if (a.out) store_rows<D, P>(a.out + r * D, v, nr, 4);
     if (a.ld) store_lds<P>(a.ld + r, ld, nr, 4);
   }
+  CNF_TRC(1);
   CNF_TR(6);
-  if constexpr (MODE == kLoss) block_sum3<kWaves * 64>(lt0, lt1, lt2, smem, a.part);
+  if constexpr (MODE == kLoss) {
+    block_sum3<kWaves * 64>(lt0, lt1, lt2, smem, a.part);
+  }
 }
 
 using KFn = void (*)(const float*, const int32_t*, const int32_t*, const float*, KArgs);
@@ -591,7 +652,9 @@ const SEntry* find(const Shape& s) {
   return nullptr;
 }
 
-size_t lds_bytes(const Shape& s, const KV& k) { return (size_t)kWaves * k.tr * s.D * 4; }
+size_t lds_bytes(const Shape& s, const KV& k) {
+  return (size_t)kWaves * k.tr * s.D * 4 * (kStage == 2 ? 2 : 1);
+}
 
 int resident_blocks(const KV& k, size_t lds) {
   static std::mutex mu;
@@ -603,6 +666,13 @@ int resident_blocks(const KV& k, size_t lds) {
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k.fn, kWaves * 64, lds) != hipSuccess ||
       n < 1)
     n = 1;
+  // at most CNF_SGPR_GRID_WPS blocks per CU even where the occupancy query
+  // allows more: at 7 per CU (forward, 71 VGPRs) the last ~10 % of a 2^20-row
+  // grid was not resident at launch and started ~18 us late (tools/sgpr_trace.py)
+#ifndef CNF_SGPR_GRID_WPS
+#define CNF_SGPR_GRID_WPS 5
+#endif
+  if (n > CNF_SGPR_GRID_WPS) n = CNF_SGPR_GRID_WPS;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
       cus < 1)
@@ -655,7 +725,9 @@ int sgpr_run(const Shape& s, const void* prepared, const float* in, float* out, 
   if (!e || !sgpr_enabled(s)) return CNF_ERR_UNSUPPORTED;
   if (B == 0) return CNF_OK;
   if (B / 128 > 0x7fffffffLL) return CNF_ERR_UNSUPPORTED;
-  if (!io_ok(in, 16) || !io_ok(out, 4) || !io_ok(all, 16) || !io_ok(ld, 4)) return CNF_ERR_UNSUPPORTED;
+  // staged tile stores write whole 16-B words: a misaligned output view stays on k_valu
+  if (!io_ok(in, 16) || !io_ok(out, kStage ? 16 : 4) || !io_ok(all, 16) || !io_ok(ld, 4))
+    return CNF_ERR_UNSUPPORTED;
   const int mode = log_priors ? kPredict : (loss_ws ? kLoss : (inverse ? kInv : kFwd));
   const KV* k = pick(e, s, mode, all != nullptr);
   if (!k) return CNF_ERR_UNSUPPORTED;
@@ -666,6 +738,12 @@ int sgpr_run(const Shape& s, const void* prepared, const float* in, float* out, 
   const float* W = reinterpret_cast<const float*>(base + idx_bytes(s)) + s.sp_region;
   KArgs a{};
   a.in = in;
+#ifdef CNF_AB_NO_Z  // A/B timing only: outputs not written
+  out = nullptr;
+#endif
+#ifdef CNF_AB_NO_LD
+  ld = nullptr;
+#endif
   a.out = out;
   a.ld = ld;
   a.all = all;
@@ -678,6 +756,10 @@ int sgpr_run(const Shape& s, const void* prepared, const float* in, float* out, 
   const int64_t nblk = grid_for(*k, s, B);
   hipLaunchKernelGGL(k->fn, dim3((unsigned)nblk), dim3(kWaves * 64), lds_bytes(s, *k), st, W,
                      inverse ? inv_q : fwd_q, flags, log_priors, a);
+  // the block-order sum of the loss records: a one-block follow-up launch.
+  // (A last-block hand-off inside k_sgpr -- agent-scope fence + counter per
+  // block -- measured 67.6 vs 35.6 us per 2^20-row call: each block's release
+  // fence writes back its XCD's whole L2.)
   if (mode == kLoss) reduce_partials(loss_ws + 4, (int)nblk, 4, 0, nullptr, loss_terms, st);
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) {
@@ -690,6 +772,11 @@ int sgpr_run(const Shape& s, const void* prepared, const float* in, float* out, 
 }  // namespace cnf
 
 #ifdef CNF_SGPR_TRACE
+extern "C" int cnf_diag_trace_clk(unsigned long long* host, int n) {
+  if (n > 16384 * 2) n = 16384 * 2;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(cnf_trace_clk), (size_t)n * 8, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? n : -1;
+}
 extern "C" int cnf_diag_trace(unsigned long long* host, int n) {
   if (n > 16384 * 8) n = 16384 * 8;
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(cnf_trace), (size_t)n * 8, 0,

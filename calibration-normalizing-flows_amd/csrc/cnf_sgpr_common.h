@@ -60,6 +60,36 @@ __device__ __forceinline__ f2 fma_clamp(float w, f2 x, f2 acc) {
   return a;
 }
 
+// acc + w * x with w = weights[idx] broadcast to both packed lanes straight
+// from the aligned SGPR pair holding it: op_sel / op_sel_hi pick that pair's
+// element for both lanes.  (A plain fma of a float weight made the compiler
+// copy each odd-indexed weight into a scratch even pair first; when the
+// scratch pair was part of the next block's in-flight s_load destination, it
+// had to wait for that load -- a full scalar-load latency inside a Linear.)
+template <int NC>
+__device__ __forceinline__ f2 fma_ws(const SW<NC>& w, int idx, f2 x, f2 acc) {
+  const f2 p = w.pair(idx & ~1);
+  f2 a;
+  if (idx & 1)
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,1,1]"
+        : "=v"(a) : "s"(p), "v"(x), "v"(acc));
+  else
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(a) : "s"(p), "v"(x), "v"(acc));
+  return a;
+}
+template <int NC>
+__device__ __forceinline__ f2 fma_ws_clamp(const SW<NC>& w, int idx, f2 x, f2 acc) {
+  const f2 p = w.pair(idx & ~1);
+  f2 a;
+  if (idx & 1)
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,1,1] clamp"
+        : "=v"(a) : "s"(p), "v"(x), "v"(acc));
+  else
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1] clamp"
+        : "=v"(a) : "s"(p), "v"(x), "v"(acc));
+  return a;
+}
+
 // Weight-block loads.  Each Linear's block arrives in SGPRs one Linear ahead:
 //   sready()          wait for the block issued one Linear ago -- a
 //                     compiler-visible s_waitcnt lgkmcnt(0), so the compiler
@@ -108,6 +138,46 @@ __device__ __forceinline__ void read_pairs(const float* sm, int lane, f2 (&v)[P]
   for (int p = 0; p < P; ++p)
 #pragma unroll
     for (int k = 0; k < D; ++k) v[p][k] = f2{b[2 * p * D + k], b[(2 * p + 1) * D + k]};
+}
+
+// Coalesced tile stores.  A lane's 2P output rows sit 2*P*D floats apart from
+// the next lane's, so storing them straight from registers makes every 16-B
+// store instruction touch 64 scattered pieces of ~40 cache lines (partial-line
+// writes the L2 must merge; measured: writing z cost 5.5 us of a 39 us cfg2
+// pass).  Instead the lane writes its rows into the wave's LDS tile (row-major,
+// the input tile's layout) and the wave stores the tile lane-linear: each
+// global_store_dwordx4 then writes 1 KiB contiguous (8 whole lines).
+template <int D, int P>
+__device__ __forceinline__ void stage_pairs(float* sm, int lane, const f2 (&v)[P][D]) {
+  float* b = sm + 2 * P * D * lane;
+#pragma unroll
+  for (int p = 0; p < P; ++p)
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      b[2 * p * D + k] = v[p][k].x;
+      b[(2 * p + 1) * D + k] = v[p][k].y;
+    }
+}
+template <int TF>
+__device__ __forceinline__ void store_tile(float* __restrict__ dst, const float* sm, int lane) {
+  constexpr int N4 = TF / 4, NI = (N4 + 63) / 64;
+  static_assert(TF % 4 == 0, "tile must be whole float4s");
+  float4 q[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+    if (N4 % 64 == 0 || i * 64 + lane < N4)
+      q[i] = *reinterpret_cast<const float4*>(sm + (i * 64 + lane) * 4);
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+    if (N4 % 64 == 0 || i * 64 + lane < N4) {
+#ifdef CNF_SGPR_NT_STORE  // A/B: streaming stores (whole lines, bypass L2 residency)
+      using v4 = __attribute__((ext_vector_type(4))) float;
+      __builtin_nontemporal_store(v4{q[i].x, q[i].y, q[i].z, q[i].w},
+                                  reinterpret_cast<v4*>(dst) + i * 64 + lane);
+#else
+      reinterpret_cast<float4*>(dst)[i * 64 + lane] = q[i];
+#endif
+    }
 }
 
 // The lane's 2*P*D output floats (pairs in logical order) to dst = its first

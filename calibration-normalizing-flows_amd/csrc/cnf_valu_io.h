@@ -227,6 +227,50 @@ __device__ __forceinline__ void block_sum3(float a, float b, float c, float* sm,
 }
 
 
+// The loss-term sums of nblk 16-B partial records by one 256-thread block
+// (threadIdx.x = t), in ONE fixed order: lane-strided sums with up to eight
+// records per lane in flight, an xor butterfly per wave, waves in index order.
+// k_reduce_rows4 (the follow-up launch) and k_sgpr's last block (the fused
+// hand-off) both sum this way, so either path gives the same bits.
+constexpr int kRR = 256;
+__device__ __forceinline__ void reduce_rows4_block(const float4* __restrict__ partials, int nblk,
+                                                   float* __restrict__ out, float (*red)[3]) {
+  const int t = threadIdx.x;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+  for (int b0 = t; b0 < nblk; b0 += 8 * kRR) {
+    float4 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int b = b0 + k * kRR;
+      v[k] = b < nblk ? partials[b] : float4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      s0 += v[k].x;
+      s1 += v[k].y;
+      s2 += v[k].z;
+    }
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    s0 += __shfl_xor(s0, off);
+    s1 += __shfl_xor(s1, off);
+    s2 += __shfl_xor(s2, off);
+  }
+  if ((t & 63) == 0) {
+    red[t >> 6][0] = s0;
+    red[t >> 6][1] = s1;
+    red[t >> 6][2] = s2;
+  }
+  __syncthreads();
+  if (t < 3) {
+    float a = 0.f;
+#pragma unroll
+    for (int w = 0; w < kRR / 64; ++w) a += red[w][t];
+    out[t] = a;
+  }
+}
+
 template <int ROWS>
 __device__ __forceinline__ void store_ld(float* ld_out, int64_t row0, int tid, int nrows, float v) {
   if (tid < nrows) ld_out[row0 + tid] = v;

@@ -35,6 +35,7 @@
 #include "cnf_valu_common.h"
 #include "cnf_sgpr_common.h"
 #include "cnf_valu_io.h"
+#include "cnf_valu_io.h"
 #include "cnf_vjp2.h"
 
 namespace cnf {
@@ -505,48 +506,12 @@ __global__ __launch_bounds__(64) void k_reduce_rows(const float* __restrict__ pa
 }
 
 // Loss-term sums of 16-B partial records ([t0, t1, t2, pad] per block, the
-// forward-loss kernels' layout): four waves, one float4 per record, up to
-// eight records per lane in flight before the first add, so a 2,048-block grid
-// is one round of load latency instead of four.  Fixed order throughout
-// (lane-strided sums, xor butterfly, waves in index order): deterministic.
-constexpr int kRR = 256;
+// forward-loss kernels' layout): one block, cnf_valu_io.h reduce_rows4_block.
+using valu::kRR;
 __global__ __launch_bounds__(kRR) void k_reduce_rows4(const float4* __restrict__ partials,
                                                       int nblk, float* __restrict__ out) {
   __shared__ float red[kRR / 64][3];
-  const int t = threadIdx.x;
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f;
-  for (int b0 = t; b0 < nblk; b0 += 8 * kRR) {
-    float4 v[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int b = b0 + k * kRR;
-      v[k] = b < nblk ? partials[b] : float4{0.f, 0.f, 0.f, 0.f};
-    }
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      s0 += v[k].x;
-      s1 += v[k].y;
-      s2 += v[k].z;
-    }
-  }
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    s0 += __shfl_xor(s0, off);
-    s1 += __shfl_xor(s1, off);
-    s2 += __shfl_xor(s2, off);
-  }
-  if ((t & 63) == 0) {
-    red[t >> 6][0] = s0;
-    red[t >> 6][1] = s1;
-    red[t >> 6][2] = s2;
-  }
-  __syncthreads();
-  if (t < 3) {
-    float a = 0.f;
-#pragma unroll
-    for (int w = 0; w < kRR / 64; ++w) a += red[w][t];
-    out[t] = a;
-  }
+  valu::reduce_rows4_block(partials, nblk, out, red);
 }
 
 using VFn = void (*)(const float*, const int32_t*, const int32_t*, const int32_t*, const float*,

@@ -54,7 +54,6 @@ using f4 = __attribute__((ext_vector_type(4))) float;
 
 constexpr int kBN = 64;      // output columns per GEMM block (2 MFMA tiles of 32)
 constexpr int kKC = 128;     // reduction chunk a wave holds in registers (16 x float4)
-constexpr int kDwCols = 64;  // gradient columns per k_wdw wave (2 MFMA tiles)
 
 inline int r8(int n) { return (n + 7) & ~7; }
 
@@ -253,21 +252,27 @@ __global__ __launch_bounds__(256, PAIR ? 3 : 4) void k_wgemm(GemmArgs ga) {
   }
 }
 
-// Weight gradients: one wave per block owns a 32 (outputs) x 32*NC (inputs and
-// the ones column) strip of one (net, Linear) job over the block's row range,
-// written into the block's partial record in state_dict layout (so the
-// reduction is one fixed-order column sum).  Both MFMA operands come straight
-// from HBM: in k-step s, lane (i, h) reads G[row][n0 + i] and
-// H[row][c0 + 32c + i] of batch row mr + 2s + h -- 128 contiguous bytes per
-// half-wave.  Out-of-range outputs read clamped addresses and are never
-// written; only the batch's last partial chunk masks rows.  The next 32 rows'
-// operands load under this chunk's MFMAs.
+// Weight gradients dW = G^T [H | 1] of every (net, Linear) job of a layer over
+// row blocks (per-block partials in state_dict layout, summed in block order
+// afterwards: deterministic).  A block of four waves owns a 128-row x
+// 128-column group of one job's dW: wave w the 32 output rows n0 = 32(4 g_n +
+// w) .. +31 and EVERY column tile of the group.  The four waves therefore
+// stream the SAME H rows at the same time (one HBM pass: the other three
+// waves' reads hit L1 / L2) and each its own 32 G columns, so each operand
+// leaves HBM once per layer.  (Round 2's one-wave blocks, one 32 x 64 tile
+// each, re-read every G column per column tile and every H column per output
+// tile: 2-4x the algorithmic bytes.)  In k-step s lane (i, h) reads
+// G[row][n0 + i] and H[row][c0 + 32c + i] of row mr + 2s + h: 128 contiguous
+// bytes per half-wave.  The next 32 rows' operands load under this chunk's
+// MFMAs.  Column tiles past the job (nct < 4) are skipped by wave-uniform
+// branches; out-of-range outputs read clamped addresses and are never written;
+// only the batch's ragged end masks rows.
 struct DwJob {
   const float* G;
   const float* H;
   int64_t ldg, ldh;
   int64_t woff, boff;  // float offsets of W[0][in_off] and b[0] in the layer record
-  int wld, N, K, tiles_k;
+  int wld, N, K, tiles_c;  // tiles_c: 32-column tiles of [H | 1] (K + 1 columns)
   int cstep;           // +1, or -1 when the kernel's input columns run reversed (legacy)
   int rrev;            // output rows reversed (legacy): row n is parameter row N_full-1-n
   int nfull;
@@ -278,59 +283,66 @@ struct DwArgs {
   int64_t M, rows, PS;
 };
 
-#ifndef CNF_DW_WPS
-#define CNF_DW_WPS 1
-#endif
-template <int NC>
-__global__ __launch_bounds__(64, CNF_DW_WPS) void k_wdw(DwArgs da) {
+constexpr int kDwCT = 4;  // column tiles per wave (128 columns)
+
+__global__ __launch_bounds__(256, 2) void k_wdw(DwArgs da) {
   const DwJob& j = da.job[blockIdx.y];
-  const int lane = threadIdx.x, i = lane & 31, h = lane >> 5;
-  const int nsub = (j.N + 31) >> 5;
-  const int ns = (int)blockIdx.z % nsub, ct = (int)blockIdx.z / nsub;
-  if (ct >= j.tiles_k) return;
-  const int n0 = ns * 32, c0 = ct * 32 * NC;
+  const int lane = threadIdx.x & 63, i = lane & 31, h = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nsub = (j.N + 31) >> 5, ncg = (j.tiles_c + kDwCT - 1) / kDwCT;
+  const int gn = (int)blockIdx.z / ncg, cg = (int)blockIdx.z % ncg;
+  const int ns = gn * 4 + w;
+  if (gn * 4 >= nsub || ns >= nsub) return;  // no __syncthreads below: waves may leave
+  const int nct = min(kDwCT, j.tiles_c - cg * kDwCT);
+  const int n0 = ns * 32, c0 = cg * 32 * kDwCT;
   const int64_t r0 = (int64_t)blockIdx.x * da.rows;
   const int64_t r1 = min(da.M, r0 + da.rows);
   if (r0 >= r1) return;
   const float* gcol = j.G + min(n0 + i, j.N - 1);
-  const float* hcol[NC];
+  const float* hcol[kDwCT];
 #pragma unroll
-  for (int c = 0; c < NC; ++c) hcol[c] = j.H + min(c0 + 32 * c + i, (int)j.ldh - 1);
-  auto load = [&](int64_t mr, float (&a)[16], float (&b)[NC][16]) {
+  for (int c = 0; c < kDwCT; ++c) hcol[c] = j.H + min(c0 + 32 * c + i, (int)j.ldh - 1);
+  auto load = [&](int64_t mr, float (&a)[16], float (&b)[kDwCT][16]) {
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const int64_t row = mr + 2 * s + h;
-      a[s] = gcol[row * j.ldg];
+    for (int s = 0; s < 16; ++s) a[s] = gcol[(mr + 2 * s + h) * j.ldg];
 #pragma unroll
-      for (int c = 0; c < NC; ++c) b[c][s] = hcol[c][row * j.ldh];
-    }
+    for (int c = 0; c < kDwCT; ++c)
+      if (c < nct) {
+#pragma unroll
+        for (int s = 0; s < 16; ++s) b[c][s] = hcol[c][(mr + 2 * s + h) * j.ldh];
+      }
   };
-  f16v acc[NC];
+  auto mfmas = [&](f16v (&acc)[kDwCT], const float (&a)[16], const float (&b)[kDwCT][16]) {
 #pragma unroll
-  for (int c = 0; c < NC; ++c) acc[c] = f16v{};
+    for (int c = 0; c < kDwCT; ++c)
+      if (c < nct) {
+#pragma unroll
+        for (int s = 0; s < 16; ++s)
+          acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[c][s], acc[c], 0, 0, 0);
+      }
+  };
+  f16v acc[kDwCT];
+#pragma unroll
+  for (int c = 0; c < kDwCT; ++c) acc[c] = f16v{};
   const int64_t rfull = r0 + (r1 - r0) / 32 * 32;  // rows in whole chunks
   if (rfull > r0) {
-    float a[16], b[NC][16];
+    float a[16], b[kDwCT][16];
     load(r0, a, b);
     for (int64_t mr = r0; mr < rfull; mr += 32) {
-      float an[16], bn[NC][16];
+      float an[16], bn[kDwCT][16];
       load(mr + 32 < rfull ? mr + 32 : mr, an, bn);
       __builtin_amdgcn_sched_barrier(0);  // next chunk's loads stay ahead of the MFMAs
-#pragma unroll
-      for (int s = 0; s < 16; ++s)
-#pragma unroll
-        for (int c = 0; c < NC; ++c)
-          acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[c][s], acc[c], 0, 0, 0);
+      mfmas(acc, a, b);
 #pragma unroll
       for (int s = 0; s < 16; ++s) {
         a[s] = an[s];
 #pragma unroll
-        for (int c = 0; c < NC; ++c) b[c][s] = bn[c][s];
+        for (int c = 0; c < kDwCT; ++c) b[c][s] = bn[c][s];
       }
     }
   }
   if (rfull < r1) {  // the batch's ragged end: rows past r1 contribute zero
-    float a[16], b[NC][16];
+    float a[16], b[kDwCT][16];
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
       const int64_t row = rfull + 2 * s + h;
@@ -338,19 +350,15 @@ __global__ __launch_bounds__(64, CNF_DW_WPS) void k_wdw(DwArgs da) {
       const int64_t rr = ok ? row : r1 - 1;
       a[s] = ok ? gcol[rr * j.ldg] : 0.f;
 #pragma unroll
-      for (int c = 0; c < NC; ++c) b[c][s] = hcol[c][rr * j.ldh];
+      for (int c = 0; c < kDwCT; ++c) b[c][s] = hcol[c][rr * j.ldh];
     }
-#pragma unroll
-    for (int s = 0; s < 16; ++s)
-#pragma unroll
-      for (int c = 0; c < NC; ++c)
-        acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[c][s], acc[c], 0, 0, 0);
+    mfmas(acc, a, b);
   }
   float* out = da.partials + (int64_t)blockIdx.x * da.PS;
 #pragma unroll
-  for (int c = 0; c < NC; ++c) {
+  for (int c = 0; c < kDwCT; ++c) {
     const int k = c0 + c * 32 + i;
-    if (k > j.K) continue;
+    if (c >= nct || k > j.K) continue;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int nn = n0 + (q & 3) + 8 * (q >> 2) + 4 * h;
@@ -1032,13 +1040,12 @@ struct Runner {
         j.woff = n * s.net_floats + lin_off(s, k) + (k == 0 ? (rin ? D - 1 - DT : DT) : 0);
         j.wld = s.units[k];
         j.boff = n * s.net_floats + lin_off(s, k) + (int64_t)s.units[k + 1] * s.units[k];
-        j.tiles_k = (j.K + 1 + kDwCols - 1) / kDwCols;
-        max_subs = std::max(max_subs, j.tiles_k * ((j.N + 31) / 32));
+        j.tiles_c = (j.K + 1 + 31) / 32;
+        max_subs = std::max(max_subs, ((j.N + 127) / 128) * ((j.tiles_c + kDwCT - 1) / kDwCT));
       }
     }
-    hipLaunchKernelGGL(k_wdw<kDwCols / 32>,
-                       dim3((unsigned)p.nkb, (unsigned)jobs, (unsigned)max_subs), dim3(64), 0, st,
-                       da);
+    hipLaunchKernelGGL(k_wdw, dim3((unsigned)p.nkb, (unsigned)jobs, (unsigned)max_subs),
+                       dim3(256), 0, st, da);
     reduce_partials(part, (int)p.nkb, (int)PS, (int)PL, grads_layer, nullptr, st);
     return CNF_OK;
   }

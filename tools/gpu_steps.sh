@@ -8,7 +8,10 @@
 #   bench        python bench.py (default line)
 #   trace        k_sgpr per-wave timeline (libcnf_hip_trace.so), loss + forward
 #   rate         tools/quick_rate.py loss / forward (2^20 and 2^23 rows)
-#   ab           tools/quick_rate.py loss for every gpurun_out/../tools/ab/lib*.so
+#   ab           tools/quick_rate.py $AB_MODE for every tools/ab/lib*.so (make ab)
+#   train        cfg2 / cfg4 fused training-step times (bench.train_step_rate)
+#   wide         cfg4 forward (k_wide) time
+#   calib        the calibrator-fit epoch variant (bench.calibrator_epoch_rate)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -28,12 +31,15 @@ for step in "$@"; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) TAILN=2 run bench 600 python bench.py ;;
     trace) run trace_loss 180 python tools/sgpr_trace.py loss && run trace_fwd 180 python tools/sgpr_trace.py forward ;;
-    rate) run rate_loss 300 python tools/quick_rate.py loss && run rate_fwd 300 python tools/quick_rate.py forward ;;
+    rate) run rate 300 python tools/quick_rate.py loss forward inverse ;;
+    train) run train 300 python -c "import json, torch, bench; d = torch.device('cuda:0'); print(json.dumps({w: bench.train_step_rate(d, w, steps=(20 if w == 'cfg2' else 5)) for w in ('cfg2', 'cfg4')}))" ;;
+    wide) run wide 300 python -c "import json, torch, bench; d = torch.device('cuda:0'); r = bench.Runner(dict(bench.WORKLOADS['cfg4']), d, 1e9); t = min(bench.kernel_only_seconds(r, 10) for _ in range(3)); print(json.dumps({'cfg4_forward_us': round(t * 1e6, 1)}))" ;;
+    calib) run calib 300 python -c "import json, torch, bench; print(json.dumps(bench.calibrator_epoch_rate(torch.device('cuda:0'))))" ;;
     ab)
       for lib in tools/ab/lib*.so; do
         [ -e "$lib" ] || continue
         n=$(basename "$lib" .so)
-        CNF_HIP_LIB=$PWD/$lib run "ab_$n" 300 python tools/quick_rate.py ${AB_MODE:-loss}
+        TAILN=${AB_TAIL:-4} CNF_HIP_LIB=$PWD/$lib run "ab_$n" 300 python tools/quick_rate.py ${AB_MODE:-loss}
       done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
