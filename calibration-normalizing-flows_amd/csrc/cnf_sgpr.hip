@@ -501,6 +501,12 @@ __global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) v
   int ntr = 0;
 #endif
   int t = gw;
+#ifdef CNF_AB_STAGGER  // A/B: later resident blocks of a CU request their first tile later
+  {
+    const int slot = (int)(((int64_t)blockIdx.x * CNF_SGPR_GRID_WPS) / gridDim.x);
+    for (int i = 0; i < slot; ++i) __builtin_amdgcn_s_sleep(CNF_AB_STAGGER);
+  }
+#endif
   if (t < nfull) wave_dma<D, TR>(sm, a.in + (int64_t)t * TF, lane);
   [[maybe_unused]] float* stg = smem + (kWaves + wv) * TF;  // kStage 2: the output tile
   f2 pz[kStage == 0 ? P : 1][D], pld[P];

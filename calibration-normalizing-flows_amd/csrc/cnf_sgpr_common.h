@@ -170,7 +170,7 @@ __device__ __forceinline__ void store_tile(float* __restrict__ dst, const float*
 #pragma unroll
   for (int i = 0; i < NI; ++i)
     if (N4 % 64 == 0 || i * 64 + lane < N4) {
-#ifdef CNF_SGPR_NT_STORE  // A/B: streaming stores (whole lines, bypass L2 residency)
+#ifndef CNF_SGPR_NO_NT  // streaming stores: whole lines that need no write-back from L2 at kernel end
       using v4 = __attribute__((ext_vector_type(4))) float;
       __builtin_nontemporal_store(v4{q[i].x, q[i].y, q[i].z, q[i].w},
                                   reinterpret_cast<v4*>(dst) + i * 64 + lane);

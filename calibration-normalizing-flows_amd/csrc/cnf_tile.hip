@@ -232,28 +232,41 @@ struct PrepSeg {
   const float* W;
   const float* b;
   int64_t dst;  // float offset in the weights region
-  int mode;     // 0: natural copy, 1: MFMA tiles, 2: compact (VALU), 3: packed (SGPR)
-  int nout_full, nin_full, in_off, nin, nout, OT, KS;
-  int rev_in, rev_out;  // legacy alternate mask, odd layer: input columns / output rows reversed
   float wmul, bmul;  // mode 3: weights / bias scale (relu clamp 2^-64, log2 e; cnf_sgpr.hip)
+  int16_t mode;      // 0: natural copy, 1: MFMA tiles, 2: compact (VALU), 3: packed (SGPR)
+  int16_t nout_full, nin_full, in_off, nin, nout, OT, KS;
+  int16_t rev_in, rev_out;  // legacy alternate mask, odd layer: input columns / output rows reversed
 };
 
-struct PrepArgs {
-  PrepSeg seg[2 * kMaxLin];
-  int nseg, layer, D, L;
-  int32_t flag;
-  int32_t fq[CNF_MAX_DIM], iq[CNF_MAX_DIM];
+// cnf_prepare's work as few launches as the kernel-argument budget allows:
+// every (layer, net, Linear, layout copy) segment is one block of k_prepare
+// (up to kPrepJobs per launch, < 4 KB of arguments), and one k_prep_idx
+// launch writes the gather tables of as many layers as fit.  (Round 2 made
+// four launches per layer: 20 per prepare of the calibrator's 5-layer flow,
+// re-run after every optimizer step.)
+constexpr int kPrepJobs = 60;
+struct PrepBatch {
+  PrepSeg seg[kPrepJobs];
+  int nseg;
+};
+constexpr int kPrepIdxInts = 900;
+struct PrepIdx {
+  int32_t v[kPrepIdxInts];  // per layer: fq[D], iq[D], flag
+  int D, L, l0, nl;
 };
 
-__global__ void k_prepare(PrepArgs a, float* __restrict__ wreg, int32_t* __restrict__ idx) {
-  if ((int)blockIdx.x == a.nseg) {
-    for (int j = threadIdx.x; j < a.D; j += blockDim.x) {
-      idx[a.layer * a.D + j] = a.fq[j];
-      idx[a.L * a.D + a.layer * a.D + j] = a.iq[j];
-    }
-    if (threadIdx.x == 0) idx[2 * a.L * a.D + a.layer] = a.flag;
-    return;
+__global__ void k_prep_idx(PrepIdx a, int32_t* __restrict__ idx) {
+  const int per = 2 * a.D + 1;
+  for (int i = threadIdx.x; i < a.nl * per; i += blockDim.x) {
+    const int l = a.l0 + i / per, j = i % per;
+    const int32_t v = a.v[i];
+    if (j < a.D) idx[l * a.D + j] = v;
+    else if (j < 2 * a.D) idx[a.L * a.D + l * a.D + (j - a.D)] = v;
+    else idx[2 * a.L * a.D + l] = v;
   }
+}
+
+__global__ void k_prepare(PrepBatch a, float* __restrict__ wreg) {
   const PrepSeg& g = a.seg[blockIdx.x];
   float* dst = wreg + g.dst;
   auto orow = [&](int o) { return g.rev_out ? g.nout_full - 1 - o : o; };
@@ -382,90 +395,86 @@ int prepare_run(const Shape& s, const float* const* params, void* prepared, hipS
   int32_t* idx = reinterpret_cast<int32_t*>(base);
   float* wreg = reinterpret_cast<float*>(base + idx_bytes(s));
   const bool tiled = s.family == Family::kTile;
+  PrepBatch batch{};
+  PrepIdx tab{};
+  tab.D = s.D;
+  tab.L = s.L;
+  auto flush_jobs = [&]() {
+    if (batch.nseg > 0)
+      hipLaunchKernelGGL(k_prepare, dim3(batch.nseg), dim3(256), 0, st, batch, wreg);
+    batch.nseg = 0;
+  };
+  auto push = [&](const PrepSeg& g) {
+    if (batch.nseg == kPrepJobs) flush_jobs();
+    batch.seg[batch.nseg++] = g;
+  };
+  auto flush_idx = [&]() {
+    if (tab.nl > 0) hipLaunchKernelGGL(k_prep_idx, dim3(1), dim3(256), 0, st, tab, idx);
+    tab.l0 += tab.nl;
+    tab.nl = 0;
+  };
+  const int per = 2 * s.D + 1;
   int pi = 0;
   for (int l = 0; l < s.L; ++l) {
-    PrepArgs a{};
-    a.layer = l;
-    a.D = s.D;
-    a.L = s.L;
-    a.nseg = 0;
+    PrepSeg segs[2 * kMaxLin];
+    int nseg = 0;
     int64_t dst = tiled ? (int64_t)l * s.tile_layer_floats
                         : (int64_t)l * s.valu_net_floats * s.nets;
     for (int net = 0; net < s.nets; ++net) {
       for (int i = 0; i < s.n_lin; ++i) {
-        PrepSeg& g = a.seg[a.nseg++];
+        PrepSeg& g = segs[nseg++];
+        g = PrepSeg{};
         g.W = params[pi++];
         g.b = params[pi++];
         if (!g.W || !g.b) return CNF_ERR_NULL;
-        g.nout_full = s.units[i + 1];
-        g.nin_full = s.units[i];
+        g.nout_full = (int16_t)s.units[i + 1];
+        g.nin_full = (int16_t)s.units[i];
         g.rev_in = g.rev_out = 0;
+        g.wmul = g.bmul = 1.f;
         if (tiled && s.alt_mask && (l & 1)) {
           g.rev_in = i == 0;
           g.rev_out = i == s.n_lin - 1;
         }
         if (tiled) {
           g.mode = 1;
-          g.in_off = s.lin_inoff[i];
-          g.nin = s.lin_nin[i];
-          g.nout = s.lin_nout[i];
-          g.OT = s.lin_OT[i];
-          g.KS = s.lin_KS[i];
+          g.in_off = (int16_t)s.lin_inoff[i];
+          g.nin = (int16_t)s.lin_nin[i];
+          g.nout = (int16_t)s.lin_nout[i];
+          g.OT = (int16_t)s.lin_OT[i];
+          g.KS = (int16_t)s.lin_KS[i];
           g.dst = dst + s.tile_lin_off[i];
         } else {
           g.mode = 2;
-          g.in_off = i == 0 ? s.DT : 0;
-          g.nin = i == 0 ? s.DC : g.nin_full;
+          g.in_off = (int16_t)(i == 0 ? s.DT : 0);
+          g.nin = (int16_t)(i == 0 ? s.DC : g.nin_full);
           g.nout = g.nout_full;
           g.dst = dst + s.valu_lin_off[i];
         }
       }
       dst += tiled ? s.tile_net_floats : s.valu_net_floats;
     }
-    const int64_t* perm = nullptr;
-    if (s.any_perm && s.perms_host) {
-      const int64_t* p = s.perms_host + (int64_t)l * s.D;
-      if (p[0] >= 0) perm = p;
-    }
-    a.flag = perm ? kFlagPerm : 0;
-    int32_t rev[CNF_MAX_DIM];
-    if (perm) {
-      for (int j = 0; j < s.D; ++j) rev[perm[j]] = j;
-    }
-    // legacy alternate mask (no data flip): the flip-based stack with odd
-    // layers' weights reversed computes flip^(l+1) of the legacy layer l
-    // output, so an odd-L stack ends with one extra flip: its last table is
-    // the identity
-    const bool unflip = s.alt_mask && (s.L & 1) && l == s.L - 1;
-    if (unflip) a.flag = kFlagPerm;
-    for (int j = 0; j < s.D; ++j) {
-      // forward: out[j] = z[perm[D-1-j]]; inverse: x_in[j] = z[D-1-rev_perm[j]]
-      a.fq[j] = unflip ? j : (perm ? (int32_t)perm[s.D - 1 - j] : s.D - 1 - j);
-      a.iq[j] = unflip ? j : (perm ? s.D - 1 - rev[j] : s.D - 1 - j);
-    }
-    hipLaunchKernelGGL(k_prepare, dim3(a.nseg + 1), dim3(256), 0, st, a, wreg, idx);
+    for (int k = 0; k < nseg; ++k) push(segs[k]);
     {
       // natural copy of the layer (state_dict order) for the reverse mode
-      PrepArgs c = a;
       int64_t d = s.plain_region + (int64_t)l * s.layer_floats;
-      for (int k = 0; k < c.nseg; ++k) {
-        PrepSeg& g = c.seg[k];
+      for (int k = 0; k < nseg; ++k) {
+        PrepSeg g = segs[k];
         g.mode = 0;
         g.dst = d;
         d += (int64_t)g.nout_full * g.nin_full + g.nout_full;
+        push(g);
       }
-      hipLaunchKernelGGL(k_prepare, dim3(c.nseg), dim3(256), 0, st, c, wreg, idx);
     }
     if (!tiled && s.sp_ok) {
       // second copy of the layer in the packed SGPR layout (no index block)
-      PrepArgs b = a;
-      int64_t d2 = s.sp_region + (int64_t)l * s.sp_net_floats * s.nets;
-      for (int k = 0; k < b.nseg; ++k) {
-        PrepSeg& g = b.seg[k];
+      const int64_t d2 = s.sp_region + (int64_t)l * s.sp_net_floats * s.nets;
+      const int64_t d3 = s.vp_region + (int64_t)l * s.sp_net_floats * s.nets;
+      for (int k = 0; k < nseg; ++k) {
+        PrepSeg g = segs[k];
         const int i = k % s.n_lin;
         g.mode = 3;
         const bool last = i == s.n_lin - 1;
-        g.nout = last ? s.DT : g.nout_full;
+        g.nout = (int16_t)(last ? s.DT : g.nout_full);
         // k_sgpr folds relu into the clamp bit: hidden outputs are kept scaled
         // by 2^-64 (so relu(a) 2^-64 = clamp(a 2^-64, 0, 1)) and the next
         // Linear's input columns undo it; the s-net (first net when scale is
@@ -476,23 +485,46 @@ int prepare_run(const Shape& s, const float* const* params, void* prepared, hipS
         g.wmul = sout / sin;
         g.bmul = sout;
         g.dst = d2 + (k / s.n_lin) * s.sp_net_floats + s.sp_lin_off[i];
-      }
-      hipLaunchKernelGGL(k_prepare, dim3(b.nseg), dim3(256), 0, st, b, wreg, idx);
-      // ... and a plain copy (no relu or log2(e) scaling) for the reverse mode
-      PrepArgs c = b;
-      const int64_t d3 = s.vp_region + (int64_t)l * s.sp_net_floats * s.nets;
-      for (int k = 0; k < c.nseg; ++k) {
-        PrepSeg& g = c.seg[k];
+        push(g);
+        // ... and a plain copy (no relu or log2(e) scaling) for the reverse mode
         g.wmul = g.bmul = 1.f;
-        g.dst = d3 + (k / s.n_lin) * s.sp_net_floats + s.sp_lin_off[k % s.n_lin];
+        g.dst = d3 + (k / s.n_lin) * s.sp_net_floats + s.sp_lin_off[i];
+        push(g);
       }
-      hipLaunchKernelGGL(k_prepare, dim3(c.nseg), dim3(256), 0, st, c, wreg, idx);
     }
-    hipError_t err = hipGetLastError();
-    if (err != hipSuccess) {
-      set_hip_error(err);
-      return CNF_ERR_HIP;
+    // gather tables of layer l
+    const int64_t* perm = nullptr;
+    if (s.any_perm && s.perms_host) {
+      const int64_t* p = s.perms_host + (int64_t)l * s.D;
+      if (p[0] >= 0) perm = p;
     }
+    int32_t flag = perm ? kFlagPerm : 0;
+    int32_t rev[CNF_MAX_DIM];
+    if (perm) {
+      for (int j = 0; j < s.D; ++j) rev[perm[j]] = j;
+    }
+    // legacy alternate mask (no data flip): the flip-based stack with odd
+    // layers' weights reversed computes flip^(l+1) of the legacy layer l
+    // output, so an odd-L stack ends with one extra flip: its last table is
+    // the identity
+    const bool unflip = s.alt_mask && (s.L & 1) && l == s.L - 1;
+    if (unflip) flag = kFlagPerm;
+    if ((tab.nl + 1) * per > kPrepIdxInts) flush_idx();
+    int32_t* v = tab.v + tab.nl * per;
+    for (int j = 0; j < s.D; ++j) {
+      // forward: out[j] = z[perm[D-1-j]]; inverse: x_in[j] = z[D-1-rev_perm[j]]
+      v[j] = unflip ? j : (perm ? (int32_t)perm[s.D - 1 - j] : s.D - 1 - j);
+      v[s.D + j] = unflip ? j : (perm ? s.D - 1 - rev[j] : s.D - 1 - j);
+    }
+    v[2 * s.D] = flag;
+    ++tab.nl;
+  }
+  flush_jobs();
+  flush_idx();
+  hipError_t err = hipGetLastError();
+  if (err != hipSuccess) {
+    set_hip_error(err);
+    return CNF_ERR_HIP;
   }
   if (tiled && s.wide_floats > 0) return wide_prepare(s, params, prepared, st);
   return CNF_OK;

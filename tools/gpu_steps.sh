@@ -41,6 +41,10 @@ for step in "$@"; do
         n=$(basename "$lib" .so)
         TAILN=${AB_TAIL:-4} CNF_HIP_LIB=$PWD/$lib run "ab_$n" 300 python tools/quick_rate.py ${AB_MODE:-loss}
       done ;;
+    prof:*)  # prof:<workload>:<mode>:<launches> -> gpurun_out/prof_<workload>_<mode>/
+      IFS=: read -r _ wl md nl <<< "$step"
+      rm -rf gpurun_out/prof_${wl}_${md}
+      run prof_${wl}_${md} 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${wl}_${md} -o run --output-format csv -- python tools/prof_target.py --workload $wl --mode $md --launches $nl ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -17,13 +17,23 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--workload", default="cfg2")
 ap.add_argument("--launches", type=int, default=40)
 ap.add_argument("--batch", type=int, default=0)
-ap.add_argument("--mode", default="loss", choices=["loss", "forward", "all", "train"])
+ap.add_argument("--mode", default="loss", choices=["loss", "forward", "all", "train", "calib"])
 a = ap.parse_args()
 w = dict(bench.WORKLOADS[a.workload])
 if a.batch:
     w["B"] = a.batch
 dev = torch.device("cuda:0")
-if a.mode == "train":
+if a.mode == "calib":  # the calibrator-fit epochs (graph replays), notebook shape
+    import numpy as np
+    import calibrators as C
+    from flows.realNVP_torch import RealNvpFlow
+    rs = np.random.RandomState(5)
+    yy = rs.randint(0, 3, size=1500)
+    xx = rs.standard_normal((1500, 3)) + 3.0 * np.eye(3)[yy]
+    cal = C.TorchFlowCalibrator(RealNvpFlow, xx, yy, layers=5, hidden_size=[3, 3],
+                                epochs=a.launches, dev=dev)
+    name = "calibrator"
+elif a.mode == "train":
     from cnf_hip import vjp as V
     flow = bench.make_flow(w, dev)
     stack = flow._native_stack()
