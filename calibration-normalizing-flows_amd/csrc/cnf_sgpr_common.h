@@ -90,6 +90,18 @@ __device__ __forceinline__ f2 fma_ws_clamp(const SW<NC>& w, int idx, f2 x, f2 ac
   return a;
 }
 
+// w * x, w = weights[idx] broadcast from its aligned SGPR pair (as fma_ws)
+template <int NC>
+__device__ __forceinline__ f2 mul_ws(const SW<NC>& w, int idx, f2 x) {
+  const f2 p = w.pair(idx & ~1);
+  f2 a;
+  if (idx & 1)
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1]" : "=v"(a) : "s"(p), "v"(x));
+  else
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(a) : "s"(p), "v"(x));
+  return a;
+}
+
 // Weight-block loads.  Each Linear's block arrives in SGPRs one Linear ahead:
 //   sready()          wait for the block issued one Linear ago -- a
 //                     compiler-visible s_waitcnt lgkmcnt(0), so the compiler

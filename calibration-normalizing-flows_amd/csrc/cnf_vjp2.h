@@ -24,7 +24,7 @@ struct VArgs2 {
   const float* gld;
   float* dx;
   float* partials;
-  float* stash;  // [L][B][D/2] transformed-half layer inputs
+  float* stash;  // [L][B][D/2] transformed-half layer inputs, (row 2i, row 2i+1) interleaved
   int64_t B;
   int L, kind;
   float det, grad_scale;
@@ -110,7 +110,7 @@ __device__ __forceinline__ void vlin(const SW<NC>& w, const f2* x, f2* y) {
 #pragma unroll
   for (int k = 1; k < NIN; ++k)
 #pragma unroll
-    for (int o = 0; o < NOUT; ++o) a[o] = fmaT(w[widx<S>(o, k)], x[k], a[o]);
+    for (int o = 0; o < NOUT; ++o) a[o] = fma_ws(w, widx<S>(o, k), x[k], a[o]);
 #pragma unroll
   for (int o = 0; o < NOUT; ++o) y[o] = RELU ? maxT(a[o], splat(0.f, f2{})) : a[o];
 }
@@ -119,39 +119,45 @@ __device__ __forceinline__ void vlin(const SW<NC>& w, const f2* x, f2* y) {
 template <int NIN, int NOUT, int S, int NC>
 __device__ __forceinline__ void vlin_t(const SW<NC>& w, const f2* gout, f2* gin) {
 #pragma unroll
-  for (int k = 0; k < NIN; ++k) gin[k] = gout[0] * splat(w[widx<S>(0, k)], f2{});
+  for (int k = 0; k < NIN; ++k) gin[k] = mul_ws(w, widx<S>(0, k), gout[0]);
 #pragma unroll
   for (int o = 1; o < NOUT; ++o)
 #pragma unroll
-    for (int k = 0; k < NIN; ++k) gin[k] = fmaT(w[widx<S>(o, k)], gout[o], gin[k]);
-}
-
-template <int NC>
-__device__ __forceinline__ void sload_now(SW<NC>& w, const float* p) {
-  sissue(w, p);
-  sready();
+    for (int k = 0; k < NIN; ++k) gin[k] = fma_ws(w, widx<S>(o, k), gout[o], gin[k]);
 }
 
 // One net's activations on the conditioning half c (plain weights): h1, h2, out.
+// Two SGPR buffers in turn: each Linear's block is issued before the previous
+// Linear's FMAs (sready / sissue, cnf_sgpr_common.h), so only the net's first
+// load waits its full latency.
 template <class S, int NC>
 __device__ __forceinline__ void vnet_fwd(const float* wn, const f2* c, f2* h1, f2* h2, f2* out) {
-  SW<NC> w;
+  SW<NC> A, Bw;
+  sissue(A, wn);
   if constexpr (S::NL == 1) {
-    sload_now(w, wn);
-    vlin<S::nin(0), S::nout(0), S::stride(0), false>(w, c, out);
+    sready();
+    vlin<S::nin(0), S::nout(0), S::stride(0), false>(A, c, out);
   } else if constexpr (S::NL == 2) {
-    sload_now(w, wn);
-    vlin<S::nin(0), S::nout(0), S::stride(0), true>(w, c, h1);
-    sload_now(w, wn + S::off(1));
-    vlin<S::nin(1), S::nout(1), S::stride(1), false>(w, h1, out);
+    sready();
+    sissue(Bw, wn + S::off(1));
+    vlin<S::nin(0), S::nout(0), S::stride(0), true>(A, c, h1);
+    sready();
+    vlin<S::nin(1), S::nout(1), S::stride(1), false>(Bw, h1, out);
   } else {
-    sload_now(w, wn);
-    vlin<S::nin(0), S::nout(0), S::stride(0), true>(w, c, h1);
-    sload_now(w, wn + S::off(1));
-    vlin<S::nin(1), S::nout(1), S::stride(1), true>(w, h1, h2);
-    sload_now(w, wn + S::off(2));
-    vlin<S::nin(2), S::nout(2), S::stride(2), false>(w, h2, out);
+    sready();
+    sissue(Bw, wn + S::off(1));
+    vlin<S::nin(0), S::nout(0), S::stride(0), true>(A, c, h1);
+    sready();
+    sissue(A, wn + S::off(2));
+    vlin<S::nin(1), S::nout(1), S::stride(1), true>(Bw, h1, h2);
+    sready();
+    vlin<S::nin(2), S::nout(2), S::stride(2), false>(A, h2, out);
   }
+}
+
+// relu' from the stored activation h (>= 0, or NaN): keeps g where h > 0
+__device__ __forceinline__ f2 relu_mask(f2 g, f2 h) {
+  return f2{h.x > 0.f ? g.x : 0.f, h.y > 0.f ? g.y : 0.f};
 }
 
 // Back-propagate one net: gout (d/d out) -> adds d/dc into gc and leaves the
@@ -161,50 +167,42 @@ __device__ __forceinline__ void vnet_bwd(const float* wn, const f2* h1, const f2
                                          const f2* gout, f2* gc, f2* G) {
   constexpr int H1 = S::NL >= 2 ? S::nout(0) : 0, H2 = S::NL == 3 ? S::nout(1) : 0;
   constexpr int DT = S::DT, DC = S::DC;
-  SW<NC> w;
+  SW<NC> A, Bw;
   f2 gin[DC];
-  const f2 zero = splat(0.f, f2{});
   if constexpr (S::NL == 1) {
-    sload_now(w, wn);
-    vlin_t<DC, DT, S::stride(0)>(w, gout, gin);
+    sissue(A, wn);
+    sready();
+    vlin_t<DC, DT, S::stride(0)>(A, gout, gin);
   } else if constexpr (S::NL == 2) {
     f2 g1[H1];
-    sload_now(w, wn + S::off(1));
-    vlin_t<H1, DT, S::stride(1)>(w, gout, g1);
+    sissue(A, wn + S::off(1));
+    sready();
+    sissue(Bw, wn);
+    vlin_t<H1, DT, S::stride(1)>(A, gout, g1);
 #pragma unroll
-    for (int m = 0; m < H1; ++m) {
-      const f2 h = h1[m];
-      g1[m] = f2{h.x > 0.f ? g1[m].x : 0.f, h.y > 0.f ? g1[m].y : 0.f};
-      G[m] = g1[m];
-    }
-    sload_now(w, wn);
-    vlin_t<DC, H1, S::stride(0)>(w, g1, gin);
+    for (int m = 0; m < H1; ++m) G[m] = g1[m] = relu_mask(g1[m], h1[m]);
+    sready();
+    vlin_t<DC, H1, S::stride(0)>(Bw, g1, gin);
   } else {
     f2 g2[H2], g1[H1];
-    sload_now(w, wn + S::off(2));
-    vlin_t<H2, DT, S::stride(2)>(w, gout, g2);
+    sissue(A, wn + S::off(2));
+    sready();
+    sissue(Bw, wn + S::off(1));
+    vlin_t<H2, DT, S::stride(2)>(A, gout, g2);
 #pragma unroll
-    for (int m = 0; m < H2; ++m) {
-      const f2 h = h2[m];
-      g2[m] = f2{h.x > 0.f ? g2[m].x : 0.f, h.y > 0.f ? g2[m].y : 0.f};
-      G[H1 + m] = g2[m];
-    }
-    sload_now(w, wn + S::off(1));
-    vlin_t<H1, H2, S::stride(1)>(w, g2, g1);
+    for (int m = 0; m < H2; ++m) G[H1 + m] = g2[m] = relu_mask(g2[m], h2[m]);
+    sready();
+    sissue(A, wn);
+    vlin_t<H1, H2, S::stride(1)>(Bw, g2, g1);
 #pragma unroll
-    for (int m = 0; m < H1; ++m) {
-      const f2 h = h1[m];
-      g1[m] = f2{h.x > 0.f ? g1[m].x : 0.f, h.y > 0.f ? g1[m].y : 0.f};
-      G[m] = g1[m];
-    }
-    sload_now(w, wn);
-    vlin_t<DC, H1, S::stride(0)>(w, g1, gin);
+    for (int m = 0; m < H1; ++m) G[m] = g1[m] = relu_mask(g1[m], h1[m]);
+    sready();
+    vlin_t<DC, H1, S::stride(0)>(A, g1, gin);
   }
 #pragma unroll
   for (int j = 0; j < DT; ++j) G[H1 + H2 + j] = gout[j];
 #pragma unroll
   for (int k = 0; k < DC; ++k) gc[k] += gin[k];
-  (void)zero;
 }
 
 // Fold G^T H of this tile's 128 rows (GS x HS <= 16 x 16) into acc: the stage
@@ -335,6 +333,7 @@ __global__ __launch_bounds__(64, 2) void k_vjp2(const float* __restrict__ W,
     const int64_t row0 = (int64_t)tix * kV2TR;
     const int64_t r = row0 + 2 * lane;
     const int nr = r >= B ? 0 : (r + 1 >= B ? 1 : 2);
+    const bool full = row0 + kV2TR <= B;  // wave-uniform: every lane holds two rows
     // ---- rows in: one tile through LDS (full tiles: 16-B loads) ----
     f2 v[D];
     if (row0 + kV2TR <= B) {
@@ -364,12 +363,18 @@ __global__ __launch_bounds__(64, 2) void k_vjp2(const float* __restrict__ W,
 #pragma unroll
       for (int k = 0; k < DC; ++k) c[k] = v[R<D, O>(DT + k)];
       f2 h1[H1 ? H1 : 1], h2[H2 ? H2 : 1], t[DT], sv[DT];
-      {  // x_T of this layer, rows r, r+1: 2*DT contiguous floats
+      {  // x_T of this layer, rows r, r+1: 2*DT contiguous floats as (row r,
+         // row r+1) pairs (8-B stores: the lane's slot starts 8-B aligned)
         float* sp = a.stash + ((int64_t)l * B + r) * DT;
+        if (full) {
 #pragma unroll
-        for (int j = 0; j < DT; ++j) {
-          if (nr > 0) sp[j] = v[R<D, O>(j)].x;
-          if (nr > 1) sp[DT + j] = v[R<D, O>(j)].y;
+          for (int j = 0; j < DT; ++j) reinterpret_cast<f2*>(sp)[j] = v[R<D, O>(j)];
+        } else {
+#pragma unroll
+          for (int j = 0; j < DT; ++j) {
+            if (nr > 0) sp[2 * j] = v[R<D, O>(j)].x;
+            if (nr > 1) sp[2 * j + 1] = v[R<D, O>(j)].y;
+          }
         }
       }
       vnet_fwd<S, NC>(wl + (NETS == 2 ? S::NF : 0), c, h1, h2, t);
@@ -492,8 +497,14 @@ __global__ __launch_bounds__(64, 2) void k_vjp2(const float* __restrict__ W,
       f2 xT[DT];
       {
         const float* sp = a.stash + ((int64_t)l * B + r) * DT;
+        if (full) {
 #pragma unroll
-        for (int j = 0; j < DT; ++j) xT[j] = f2{nr > 0 ? sp[j] : 0.f, nr > 1 ? sp[DT + j] : 0.f};
+          for (int j = 0; j < DT; ++j) xT[j] = reinterpret_cast<const f2*>(sp)[j];
+        } else {
+#pragma unroll
+          for (int j = 0; j < DT; ++j)
+            xT[j] = f2{nr > 0 ? sp[2 * j] : 0.f, nr > 1 ? sp[2 * j + 1] : 0.f};
+        }
       }
       f2 th1[H1 ? H1 : 1], th2[H2 ? H2 : 1], t[DT];
       vnet_fwd<S, NC>(wl + (NETS == 2 ? S::NF : 0), c, th1, th2, t);
@@ -515,8 +526,10 @@ __global__ __launch_bounds__(64, 2) void k_vjp2(const float* __restrict__ W,
         }
         f2 G[GS];
         vnet_bwd<S, NC>(wl, sh1, sh2, gs, gc, G);
+        if (!full) {
 #pragma unroll
-        for (int f = 0; f < GS; ++f) G[f] *= keep;
+          for (int f = 0; f < GS; ++f) G[f] *= keep;
+        }
 #pragma unroll
         for (int m = 0; m < H1; ++m) H[DC + m] = sh1[m];
 #pragma unroll
@@ -529,8 +542,10 @@ __global__ __launch_bounds__(64, 2) void k_vjp2(const float* __restrict__ W,
 #pragma unroll
         for (int j = 0; j < DT; ++j) gt[j] = g[R<D, Oi>(j)];
         vnet_bwd<S, NC>(wl + (NETS == 2 ? S::NF : 0), th1, th2, gt, gc, G);
+        if (!full) {
 #pragma unroll
-        for (int f = 0; f < GS; ++f) G[f] *= keep;
+          for (int f = 0; f < GS; ++f) G[f] *= keep;
+        }
 #pragma unroll
         for (int m = 0; m < H1; ++m) H[DC + m] = th1[m];
 #pragma unroll

@@ -5,7 +5,7 @@
 # fault / abort / timeout ends the script (exit codes other than 0, 1).
 # Usage: bash tools/gpu_check.sh [tag] [quick]
 set -u
-TAG=${1:-r02}
+TAG=${1:-r03}
 QUICK=${2:-}
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
