@@ -77,6 +77,7 @@ struct GemmJob {
 struct GemmArgs {
   GemmJob job[2];  // one per conditioner net (grid.z)
   int64_t M;
+  int ny;          // column blocks; grid.x = row groups (a multiple of 8) x ny
 };
 
 // A's reduction chunk [kc, kc + 128) of one 32-row panel (lane: row r, half
@@ -136,10 +137,17 @@ __device__ __forceinline__ void panel_mfma(f16v (&acc)[4], const f4 (&a)[16], co
 template <bool BT, int EPI, bool PAIR, int NC>
 __global__ __launch_bounds__(256, PAIR ? 3 : 4) void k_wgemm(GemmArgs ga) {
   const GemmJob& j = ga.job[blockIdx.z];
+  // XCD-aware block order: consecutive block ids go to the 8 XCDs in turn, so
+  // the ny column blocks of one row group get ids 8 apart -- the same XCD,
+  // dispatched back to back -- and the second read of each A panel hits that
+  // XCD's L2 instead of HBM (round 2's (x, y) grid read A once per column
+  // block from HBM)
+  const int bx = (int)blockIdx.x, xcd = bx & 7, q8 = bx >> 3;
+  const int by = q8 % ga.ny, rg = (q8 / ga.ny) * 8 + xcd;
   extern __shared__ __attribute__((aligned(16))) float Ws[];
   const int t = threadIdx.x, lane = t & 63, r = lane & 31, h = lane >> 5;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int n0 = blockIdx.y * kBN, N = j.N, K = j.K;
+  const int n0 = by * kBN, N = j.N, K = j.K;
   constexpr int Nt = NC * 32, ST = Nt + 8;
   const int Kp = (K + 7) & ~7;
   // weight slice -> LDS, 8 loads in flight per thread (a dependent load-store
@@ -177,7 +185,8 @@ __global__ __launch_bounds__(256, PAIR ? 3 : 4) void k_wgemm(GemmArgs ga) {
     }
   }
   __syncthreads();
-  const int64_t M = ga.M, panels = (M + 31) >> 5, stride = (int64_t)gridDim.x * 4;
+  const int64_t M = ga.M, panels = (M + 31) >> 5,
+                stride = (int64_t)(gridDim.x / ga.ny) * 4;  // row groups x 4 waves
   // a lane's output columns are fixed for the whole launch: its biases are
   // loaded once, not after each panel's stores (j.bias may alias j.C as far as
   // the compiler knows, which would hold every panel's bias load behind them)
@@ -233,7 +242,7 @@ __global__ __launch_bounds__(256, PAIR ? 3 : 4) void k_wgemm(GemmArgs ga) {
       }
     }
   };
-  int64_t pn = (int64_t)blockIdx.x * 4 + w;
+  int64_t pn = (int64_t)rg * 4 + w;
   for (; pn < panels; pn += stride) {
     f16v acc[4];
 #pragma unroll
@@ -286,7 +295,9 @@ struct DwArgs {
 constexpr int kDwCT = 4;  // column tiles per wave (128 columns)
 
 __global__ __launch_bounds__(256, 2) void k_wdw(DwArgs da) {
-  const DwJob& j = da.job[blockIdx.y];
+  // the job's fields once, into scalar registers (a reference into the
+  // argument block indexed by blockIdx.y reloads every field at every use)
+  const DwJob j = da.job[blockIdx.y];
   const int lane = threadIdx.x & 63, i = lane & 31, h = lane >> 5;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nsub = (j.N + 31) >> 5, ncg = (j.tiles_c + kDwCT - 1) / kDwCT;
@@ -298,18 +309,31 @@ __global__ __launch_bounds__(256, 2) void k_wdw(DwArgs da) {
   const int64_t r0 = (int64_t)blockIdx.x * da.rows;
   const int64_t r1 = min(da.M, r0 + da.rows);
   if (r0 >= r1) return;
-  const float* gcol = j.G + min(n0 + i, j.N - 1);
-  const float* hcol[kDwCT];
+  // operand addresses: buffer loads from a wave-uniform descriptor based at
+  // the chunk's first row (scalar arithmetic), a per-lane 32-bit byte offset
+  // fixed for the whole launch (row h of the pair, column n0 + i / c0 + 32c +
+  // i, clamped in-row) and a scalar offset per row pair -- no per-load vector
+  // address arithmetic
+  const int ldg = (int)j.ldg, ldh = (int)j.ldh;
+  const int goff = (h * ldg + min(n0 + i, j.N - 1)) * 4;
+  int hoff[kDwCT];
 #pragma unroll
-  for (int c = 0; c < kDwCT; ++c) hcol[c] = j.H + min(c0 + 32 * c + i, (int)j.ldh - 1);
+  for (int c = 0; c < kDwCT; ++c) hoff[c] = (h * ldh + min(c0 + 32 * c + i, ldh - 1)) * 4;
   auto load = [&](int64_t mr, float (&a)[16], float (&b)[kDwCT][16]) {
+    const auto gr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(j.G + mr * ldg), 0,
+                                                      0x7fffffff, 0x00020000);
+    const auto hr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(j.H + mr * ldh), 0,
+                                                      0x7fffffff, 0x00020000);
 #pragma unroll
-    for (int s = 0; s < 16; ++s) a[s] = gcol[(mr + 2 * s + h) * j.ldg];
+    for (int s = 0; s < 16; ++s)
+      a[s] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(gr, goff, 2 * s * ldg * 4, 0));
 #pragma unroll
     for (int c = 0; c < kDwCT; ++c)
       if (c < nct) {
 #pragma unroll
-        for (int s = 0; s < 16; ++s) b[c][s] = hcol[c][(mr + 2 * s + h) * j.ldh];
+        for (int s = 0; s < 16; ++s)
+          b[c][s] = __builtin_bit_cast(
+              float, __builtin_amdgcn_raw_buffer_load_b32(hr, hoff[c], 2 * s * ldh * 4, 0));
       }
   };
   auto mfmas = [&](f16v (&acc)[kDwCT], const float (&a)[16], const float (&b)[kDwCT][16]) {
@@ -343,14 +367,16 @@ __global__ __launch_bounds__(256, 2) void k_wdw(DwArgs da) {
   }
   if (rfull < r1) {  // the batch's ragged end: rows past r1 contribute zero
     float a[16], b[kDwCT][16];
+    const float* G = j.G;
+    const float* H = j.H;
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
       const int64_t row = rfull + 2 * s + h;
       const bool ok = row < r1;
       const int64_t rr = ok ? row : r1 - 1;
-      a[s] = ok ? gcol[rr * j.ldg] : 0.f;
+      a[s] = ok ? G[rr * ldg + min(n0 + i, j.N - 1)] : 0.f;
 #pragma unroll
-      for (int c = 0; c < kDwCT; ++c) b[c][s] = hcol[c][rr * j.ldh];
+      for (int c = 0; c < kDwCT; ++c) b[c][s] = H[rr * ldh + min(c0 + 32 * c + i, ldh - 1)];
     }
     mfmas(acc, a, b);
   }
@@ -852,14 +878,15 @@ void launch_nc(bool bt, int epi, bool pair, dim3 grid, size_t lds, hipStream_t s
 }
 
 // One GEMM launch over B rows; cols = columns written (N plus pad).
-void gemm(const GemmArgs& ga, int64_t B, int cols, int K, int nz, bool bt, int epi, bool pair,
+void gemm(GemmArgs ga, int64_t B, int cols, int K, int nz, bool bt, int epi, bool pair,
           hipStream_t st) {
   const unsigned ny = (unsigned)((cols + kBN - 1) / kBN);
   const size_t lds = gemm_lds(cols, K, pair);
   const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(4, 160 * 1024 / lds));
   const int64_t want = std::max<int64_t>(1, (int64_t)256 * per_cu / (ny * nz));
-  const unsigned nx = (unsigned)std::min<int64_t>(want, ((B + 31) / 32 + 3) / 4);
-  const dim3 grid(nx, ny, (unsigned)nz);
+  const int64_t nx = (std::min<int64_t>(want, ((B + 31) / 32 + 3) / 4) + 7) / 8 * 8;
+  const dim3 grid((unsigned)(nx * ny), 1, (unsigned)nz);
+  ga.ny = (int)ny;
   switch (gemm_nc(cols)) {
     case 1: launch_nc<1>(bt, epi, pair, grid, lds, st, ga); break;
     case 2: launch_nc<2>(bt, epi, pair, grid, lds, st, ga); break;
