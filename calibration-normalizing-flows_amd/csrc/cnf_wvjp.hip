@@ -87,12 +87,23 @@ struct GemmArgs {
 // stay inside the row and meet zero weight rows past K; a group past the row
 // (only in a chunk's unused tail) reads a clamped in-row address.  No lane branches, no use of a
 // loaded value before the MFMAs: the loads stay in flight.
+// Buffer loads from a descriptor based at the panel's first row (wave-uniform,
+// scalar arithmetic) with ONE per-lane byte offset: group g's 32 g bytes fold
+// into the instruction's immediate offset, so the 16 loads cost no vector
+// address arithmetic.  Groups past the row read the next row's floats (never
+// used: they meet no MFMA); past the matrix's last row the descriptor's range
+// check returns zeros.
 __device__ __forceinline__ void load_panel(f4 (&a)[16], const float* __restrict__ A, int64_t lda,
-                                           int64_t row, int64_t M, int kc, int kmax, int h) {
-  const float* arow = A + (row < M ? row : M - 1) * lda;
+                                           int64_t row0, int64_t M, int r, int kc, int h) {
+  const int64_t rows = M - row0;  // rows left in the matrix from the panel's first
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(A + row0 * lda), 0,
+      (int)std::min<int64_t>(rows * lda * 4, 0x7fffffff), 0x00020000);
+  const int rr = r < rows ? r : (int)rows - 1;  // rows past M read the last row
+  const int off = (rr * (int)lda + kc + 4 * h) * 4;
 #pragma unroll
   for (int g = 0; g < 16; ++g)
-    a[g] = *reinterpret_cast<const f4*>(arow + min(kc + 8 * g + 4 * h, kmax));
+    a[g] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 32 * g, 0, 0));
 }
 
 // acc[c] += A_panel . W[kc.., c-th 32 columns] for the chunk's ng groups; the
@@ -253,7 +264,7 @@ __global__ __launch_bounds__(256, PAIR ? 3 : 4) void k_wgemm(GemmArgs ga) {
       const int64_t lda = q ? j.lda2 : j.lda;
       for (int kc = 0; kc < Kp; kc += kKC) {
         f4 a[16];
-        load_panel(a, A, lda, pn * 32 + r, M, kc, (int)(lda - 4), h);
+        load_panel(a, A, lda, pn * 32, M, r, kc, h);
         panel_mfma<NC>(acc, a, Ws + q * Kp * ST, ST, kc, min(16, (Kp - kc) >> 3), r, h);
       }
     }

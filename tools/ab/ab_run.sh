@@ -1,8 +1,8 @@
 #!/bin/bash
-# A/B of experimental library builds: tools/ab_run.sh <script> <variant>...
+# A/B of experimental library builds: tools/ab/ab_run.sh <script> <variant>...
 # (each variant = cnf_hip/libcnf_hip_<variant>.so), one JSON line each.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 S=$1; shift
 for v in "$@"; do
