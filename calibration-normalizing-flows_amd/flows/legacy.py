@@ -44,11 +44,20 @@ model, code-old/nice.py:232-245, applies the coupling functions in FORWARD
 order with the reversed mask sequence -- it inverts only when every f_l is the
 same function; that quirk is not reproduced.)
 
-Versions 1 and 2 keep Keras' half-width conditioners (the torch restatement is
-their only implementation; on a ROCm device they run torch ops, reported
-through flows.flows._not_native).  Version 3 is the alternate-mask stack of the
-RealNVP path with the s-net absent, so it runs natively as CNF_OPT_ALT_MASK on
-the shift-only kernels.
+Versions 1 and 2 keep Keras' half-width conditioners and run natively by
+zero-embedding them into the maintained NICE layer (_EmbeddedNice):
+* version 2: its layer IS the maintained additive layer (x1 += f(x2) on the
+  first D//2 features, conditioned on the rest, then a full reversal) whose
+  t-net's first Linear sees only the conditioning columns and whose last
+  Linear's transformed rows are f's; one more reversal ends an odd-L stack;
+* version 1 (even D): with R the full reversal, a split layer in 'odd' mode
+  is M_g(R x) and in 'even' mode R M_f(x), where M is the maintained layer and
+  g is f with its input columns and output rows reversed; the stack is
+  R^[L even] M_{f_{L-1}} ... M_{f_1} M_{g_0} (R x).
+Odd-D version 1 (its 'odd' layers transform the larger half) keeps the torch
+restatement, reported through flows.flows._not_native.  Version 3 is the
+alternate-mask stack of the RealNVP path with the s-net absent, so it runs
+natively as CNF_OPT_ALT_MASK on the shift-only kernels.
 """
 import torch
 import torch.nn.functional as F
@@ -224,6 +233,7 @@ class LegacySplitCoupling(nn.Module):
         self.activation = activation
         h = dim // 2
         n_in, n_out = (h, dim - h) if mode == "odd" else (dim - h, h)
+        self.f_hidden = list(hidden_size)
         self.f = _mlp(n_in, list(hidden_size), n_out, _ACT[activation])
 
     def _couple(self, x, sign):
@@ -281,6 +291,152 @@ class LegacyAddCoupling(nn.Module):
         return x, torch.zeros(y.shape[0], dtype=y.dtype, device=y.device)
 
 
+class _Lin:
+    """What CouplingStack reads of an nn.Linear: .weight, .bias."""
+
+    def __init__(self, weight, bias):
+        self.weight, self.bias = weight, bias
+
+
+class _Net:
+    def __init__(self, lins):
+        self.layers = lins
+
+
+class _VirtualLayer:
+    """A maintained NICE layer (flows/flows.py:68-126 with scale=False) as
+    CouplingStack reads it, over zero-embedded full-width t-net tensors."""
+
+    def __init__(self, dim, hidden, lins):
+        self.dim, self.hidden_size = dim, list(hidden)
+        self.scale, self.shift, self.random_flip = False, True, False
+        self.s, self.t = None, _Net(lins)
+
+
+class _EmbeddedNice:
+    """Native plumbing of LegacyNiceFlow versions 1 / 2 (see the module
+    docstring): full-width first / last t-net Linears kept in device buffers,
+    refreshed from the half-width Keras conditioners whenever one of their
+    parameters changed (in-place version counters); hidden Linears are the
+    conditioners' own tensors.  rev[l]: layer l's conditioner enters with its
+    input columns and output rows reversed (version 1, even layers)."""
+
+    def __init__(self, flow, device):
+        self.flow = flow
+        D, h = flow.dim, flow.dim // 2
+        self.D, self.h = D, h
+        self.rev = [flow.version == 1 and l % 2 == 0 for l in range(len(flow.layers))]
+        vls, self.fparams, self.bufs = [], [], []
+        for ly in flow.layers:
+            lins = list(ly.f)
+            first, last = lins[0], lins[-1]
+            bL = torch.zeros(D, device=device)
+            if len(lins) > 1:
+                W0 = torch.zeros(first.weight.shape[0], D, device=device)
+                WL = torch.zeros(D, last.weight.shape[1], device=device)
+                vl = [_Lin(W0, first.bias)] + [_Lin(l.weight, l.bias) for l in lins[1:-1]]
+                vl.append(_Lin(WL, bL))
+            else:  # no hidden layer: ONE Linear, embedded on both sides
+                W0 = torch.zeros(D, D, device=device)
+                WL = None
+                vl = [_Lin(W0, bL)]
+            vls.append(_VirtualLayer(D, ly.f_hidden, vl))
+            self.bufs.append((W0, WL, bL))
+            self.fparams.extend([l.weight for l in lins] + [l.bias for l in lins])
+        from cnf_hip.engine import CouplingStack
+        self.stack = CouplingStack(vls)
+        self._key = None
+
+    def key(self):
+        return tuple((p.data_ptr(), p._version) for p in self.fparams)
+
+    @torch.no_grad()
+    def refresh(self):
+        k = self.key()
+        if k == self._key:
+            return
+        h = self.h
+        for ly, (W0, WL, bL), rev in zip(self.flow.layers, self.bufs, self.rev):
+            lins = list(ly.f)
+            first, last = lins[0], lins[-1]
+            if len(lins) > 1:
+                W0[:, h:].copy_(first.weight.flip(1) if rev else first.weight)
+                WL[:h].copy_(last.weight.flip(0) if rev else last.weight)
+                bL[:h].copy_(last.bias.flip(0) if rev else last.bias)
+            else:
+                w = first.weight.flip(0).flip(1) if rev else first.weight
+                W0.zero_()
+                W0[:h, h:].copy_(w)
+                bL.zero_()
+                bL[:h].copy_(first.bias.flip(0) if rev else first.bias)
+        self._key = k
+
+    def grads_back(self, flat):
+        """Flat gradient of the virtual stack (ABI order) -> per-parameter
+        gradients of the Keras conditioners (fparams order)."""
+        h = self.h
+        out_w, out_b = [], []
+        off = 0
+        for ly, rev in zip(self.flow.layers, self.rev):
+            lins = list(ly.f)
+            gw, gb = [], []
+            for i, lin in enumerate(lins):
+                n_out_full = self.D if (i == len(lins) - 1) else lin.weight.shape[0]
+                n_in_full = self.D if i == 0 else lin.weight.shape[1]
+                W = flat[off:off + n_out_full * n_in_full].view(n_out_full, n_in_full)
+                off += n_out_full * n_in_full
+                b = flat[off:off + n_out_full]
+                off += n_out_full
+                if i == 0:
+                    W = W[:, h:]
+                if i == len(lins) - 1:
+                    W, b = W[:h], b[:h]
+                if rev and i == 0:
+                    W = W.flip(1)
+                if rev and i == len(lins) - 1:
+                    W, b = W.flip(0), b.flip(0)
+                gw.append(W.contiguous())
+                gb.append(b.contiguous())
+            out_w.extend(gw)
+            out_b.extend(gb)
+        # fparams order per layer: weights then biases
+        res, iw, ib = [], 0, 0
+        for ly in self.flow.layers:
+            n = len(list(ly.f))
+            res.extend(out_w[iw:iw + n] + out_b[ib:ib + n])
+            iw += n
+            ib += n
+        return res
+
+
+class _EmbedFn(torch.autograd.Function):
+    """The virtual stack's transform (inverse=False) or inverse as one native
+    launch, gradients through cnf_vjp / cnf_vjp_inverse mapped back onto the
+    half-width conditioners."""
+
+    @staticmethod
+    def forward(ctx, emb, inverse, x, *fparams):
+        emb.refresh()
+        fin, ld, _ = emb.stack.run(x, inverse=inverse)
+        ctx.emb, ctx.inverse, ctx.key = emb, inverse, emb.key()
+        ctx.save_for_backward(x)
+        return fin, ld
+
+    @staticmethod
+    def backward(ctx, g_out, g_ld):
+        from cnf_hip.vjp import stack_vjp, stack_vjp_inverse
+        (x,) = ctx.saved_tensors
+        emb = ctx.emb
+        if emb.key() != ctx.key:
+            raise RuntimeError("one of the variables needed for gradient computation has been "
+                               "modified by an inplace operation: a legacy NICE conditioner "
+                               "changed between the native pass and its backward")
+        fn = stack_vjp_inverse if ctx.inverse else stack_vjp
+        dx, grads = fn(emb.stack, x, g_out, g_ld, False, ctx.needs_input_grad[2])
+        flat = torch.cat([g.reshape(-1) for g in grads])
+        return (None, None, dx) + tuple(emb.grads_back(flat))
+
+
 class LegacyNiceFlow(nn.Module):
     """The NICE flows of code-old/nice.py in torch (see the module docstring):
     version 1 `NiceFlow`, 2 `NiceFlow_v2`, 3 `NiceFlow_v3`; default hidden
@@ -305,16 +461,17 @@ class LegacyNiceFlow(nn.Module):
         self.layers = nn.ModuleList(mods)
         self.invertible = True
         self._stack = None
+        self._emb = None
 
-    # -- native plumbing (version 3) ---------------------------------------
+    # -- native plumbing ---------------------------------------------------
     def _native_ok(self, x):
         if not (isinstance(x, torch.Tensor) and x.is_cuda and x.dtype == torch.float32
                 and x.dim() == 2 and x.shape[1] == self.dim):
             return False
         from flows.flows import _not_native
-        if self.version != 3:
-            _not_native("legacy NiceFlow version %d (half-width split conditioners)"
-                        % self.version)
+        if self.version == 1 and self.dim % 2:
+            _not_native("legacy NiceFlow version 1 with odd D (its 'odd' layers transform "
+                        "the larger half)")
             return False
         if self.layers[0].activation != "relu":
             _not_native("legacy NICE activation %r" % self.layers[0].activation)
@@ -328,12 +485,40 @@ class LegacyNiceFlow(nn.Module):
             self._stack = CouplingStack(list(self.layers), options=_lib.OPT_ALT_MASK)
         return self._stack
 
+    def _embedded(self, device):
+        emb = self._emb
+        if emb is None or emb.bufs[0][0].device != device:
+            emb = self._emb = _EmbeddedNice(self, device)
+        return emb
+
+    def _native_split(self, x, inverse):
+        """Versions 1 / 2 on the virtual maintained stack (module docstring)."""
+        emb = self._embedded(x.device)
+        L = len(self.layers)
+        pre = self.version == 1          # R before the stack (after, for the inverse)
+        post = (self.version == 1 and L % 2 == 0) or (self.version == 2 and L % 2 == 1)
+        if inverse:
+            pre, post = post, pre
+        if pre:
+            x = x.flip(1)
+        fparams = emb.fparams
+        if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in fparams)):
+            y, ld = _EmbedFn.apply(emb, inverse, x.contiguous(), *fparams)
+        else:
+            emb.refresh()
+            y, ld, _ = emb.stack.run(x.contiguous(), inverse=inverse)
+        if post:
+            y = y.flip(1)
+        return y, ld
+
     def invalidate_native(self):
         self._stack = None
+        self._emb = None
 
     def __getstate__(self):
         st = self.__dict__.copy()
         st["_stack"] = None
+        st["_emb"] = None
         return st
 
     @staticmethod
@@ -341,7 +526,12 @@ class LegacyNiceFlow(nn.Module):
         return x.flip(1)  # ReIndex() with the default index (code-old/nice.py:38-51)
 
     def forward(self, x):
-        if self._native_ok(x):
+        if self._native_ok(x) and self.version != 3:
+            try:
+                return self._native_split(x, inverse=False)
+            except UnsupportedShape as e:
+                _not_native("legacy NICE %s" % e)
+        elif self._native_ok(x):
             try:
                 stack = self._native_stack()
                 if torch.is_grad_enabled() and (x.requires_grad or stack.requires_grad()):
@@ -363,7 +553,12 @@ class LegacyNiceFlow(nn.Module):
         return x, ld
 
     def backward(self, y):
-        if self._native_ok(y):
+        if self._native_ok(y) and self.version != 3:
+            try:
+                return self._native_split(y, inverse=True)
+            except UnsupportedShape as e:
+                _not_native("legacy NICE %s" % e)
+        elif self._native_ok(y):
             try:
                 stack = self._native_stack()
                 if torch.is_grad_enabled() and (y.requires_grad or stack.requires_grad()):

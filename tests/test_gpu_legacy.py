@@ -117,22 +117,81 @@ def test_legacy_nice_v3_native_matches_restatement(D, L, hidden):
     assert (xg.grad.cpu() - gx_ref).abs().max().item() / sc <= 1e-4
 
 
-def test_legacy_nice_split_versions_report_torch_execution():
-    """NiceFlow / NiceFlow_v2 keep Keras' half-width conditioners: on the GPU
-    they run torch ops and say so (RuntimeWarning, or an error under
-    CNF_STRICT_NATIVE), with results equal to the CPU restatement."""
+@pytest.mark.parametrize("version,D,L,hidden", [
+    (1, 10, 4, [10]),     # code-old/nice.py NiceFlow defaults: hidden [dim], layers 4
+    (1, 6, 3, [5, 5]),    # odd L: one more reversal
+    (1, 4, 2, []),        # one Linear per conditioner
+    (2, 10, 4, [10]),     # NiceFlow_v2
+    (2, 7, 3, [5, 5]),    # odd D, odd L
+    (2, 3, 2, []),
+])
+def test_legacy_nice_split_versions_native(version, D, L, hidden):
+    """NiceFlow / NiceFlow_v2 (code-old/nice.py:101-212) natively: the
+    half-width Keras conditioners zero-embedded into the maintained additive
+    layer (flows/legacy.py _EmbeddedNice).  Forward, inverse and every
+    gradient vs the CPU torch restatement (parity unpinned: TensorFlow
+    absent)."""
     from flows.legacy import LegacyNiceFlow
-    for version in (1, 2):
-        torch.manual_seed(0)
-        f = LegacyNiceFlow(10, layers=3, version=version)
-        x = torch.randn(64, 10)
+    torch.manual_seed(0)
+    f = LegacyNiceFlow(D, layers=L, hidden_size=hidden, version=version)
+    g = torch.Generator().manual_seed(1)
+    with torch.no_grad():
+        for p in f.parameters():
+            p.copy_(torch.randn(p.shape, generator=g) * 0.2)
+    x = torch.randn(257, D, generator=torch.Generator().manual_seed(3))
+    w = torch.randn(257, D, generator=torch.Generator().manual_seed(4))
+    with torch.no_grad():
+        y_ref, _ = f(x)
+        x_back, _ = f.backward(y_ref)
+    xc = x.clone().requires_grad_(True)
+    (f(xc)[0] * w).sum().backward()
+    g_ref = {k: p.grad.clone() for k, p in f.named_parameters()}
+    gx_ref = xc.grad.clone()
+
+    fg = f.to(DEV)
+    n0 = engine.stats["forward"] + engine.stats["inverse"]
+    with torch.no_grad():
+        y, ld = fg(x.to(DEV))
+        xb, ild = fg.backward(y_ref.to(DEV))
+    assert engine.stats["forward"] + engine.stats["inverse"] >= n0 + 2, "native path did not run"
+    assert _rel(y.cpu(), y_ref) <= 1e-5 and _rel(xb.cpu(), x_back) <= 1e-5
+    assert ld.abs().max().item() == 0 and ild.abs().max().item() == 0
+    fg.zero_grad()
+    v0 = engine.stats["vjp"]
+    xg = x.to(DEV).requires_grad_(True)
+    (fg(xg)[0] * w.to(DEV)).sum().backward()
+    assert engine.stats["vjp"] > v0, "native reverse mode did not run"
+    for k, p in fg.named_parameters():
+        sc = g_ref[k].abs().max().item() + 1e-3
+        assert (p.grad.cpu() - g_ref[k]).abs().max().item() / sc <= 1e-4, k
+    sc = gx_ref.abs().max().item() + 1e-3
+    assert (xg.grad.cpu() - gx_ref).abs().max().item() / sc <= 1e-4
+    # an optimizer-style in-place update reaches the kernels
+    with torch.no_grad():
+        for p in fg.parameters():
+            p.mul_(0.5)
+        y2, _ = fg(x.to(DEV))
+    f2 = LegacyNiceFlow(D, layers=L, hidden_size=hidden, version=version)
+    f2.load_state_dict({k: v.cpu() for k, v in fg.state_dict().items()})
+    with torch.no_grad():
+        y2_ref, _ = f2(x)
+    assert _rel(y2.cpu(), y2_ref) <= 1e-5
+
+
+def test_legacy_nice_v1_odd_dim_reports_torch_execution():
+    """NiceFlow (version 1) with odd D transforms the larger half in its 'odd'
+    layers, which the maintained layer cannot express: it runs torch ops on
+    the GPU and says so, with results equal to the CPU restatement."""
+    from flows.legacy import LegacyNiceFlow
+    import flows.flows as FF
+    torch.manual_seed(0)
+    f = LegacyNiceFlow(7, layers=3, version=1)
+    x = torch.randn(64, 7)
+    with torch.no_grad():
+        y_ref, _ = f(x)
+    fg = f.to(DEV)
+    FF._warned.clear()
+    with pytest.warns(RuntimeWarning, match="version 1 with odd D"):
         with torch.no_grad():
-            y_ref, _ = f(x)
-        fg = f.to(DEV)
-        with pytest.warns(RuntimeWarning, match="legacy NiceFlow version"):
-            import flows.flows as FF
-            FF._warned.discard("legacy NiceFlow version %d (half-width split conditioners)"
-                               % version)
-            with torch.no_grad():
-                y, _ = fg(x.to(DEV))
-        assert _rel(y.cpu(), y_ref) <= 1e-5
+            y, _ = fg(x.to(DEV))
+    assert _rel(y.cpu(), y_ref) <= 1e-5

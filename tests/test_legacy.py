@@ -187,3 +187,44 @@ def test_nice_factory_legacy_option():
     assert isinstance(g, NiceFlow) and not isinstance(g, LegacyNiceFlow)
     with pytest.raises(ValueError):
         NiceFlow(6, legacy=4)
+
+
+@pytest.mark.parametrize("version,D,L,hidden", [(1, 4, 1, []), (1, 6, 4, [5]), (1, 10, 3, [4, 3]),
+                                                (2, 3, 1, []), (2, 5, 2, [5]), (2, 10, 3, [4, 3])])
+def test_legacy_nice_split_equals_embedded_maintained_stack(version, D, L, hidden):
+    """The identity the native NiceFlow / NiceFlow_v2 path rests on (flows/
+    legacy.py _EmbeddedNice), in float64 on the CPU: the split coupling stack
+    equals the maintained additive stack (mask on the first D//2 features,
+    flip after every layer) over the zero-embedded conditioners -- version 1
+    with each even layer's conditioner reversed and one reversal before the
+    stack (after it too for even L), version 2 with one reversal after an
+    odd-L stack."""
+    from flows.legacy import LegacyNiceFlow, _EmbeddedNice
+    torch.manual_seed(0)
+    f = LegacyNiceFlow(D, layers=L, hidden_size=hidden, version=version).double()
+    with torch.no_grad():
+        for p in f.parameters():
+            p.copy_(torch.randn_like(p) * 0.3)
+    x = torch.randn(7, D, dtype=torch.float64)
+    with torch.no_grad():
+        y_ref, _ = f(x)
+        emb = _EmbeddedNice(f, "cpu")
+        for bufs in emb.bufs:
+            for t in bufs:
+                if t is not None:
+                    t.data = t.data.double()
+        emb.refresh()
+        z = x.flip(1) if version == 1 else x
+        h = D // 2
+        mask = torch.zeros(1, D, dtype=torch.float64)
+        mask[:, h:] = 1
+        for vl in emb.stack.layers:
+            a = mask * z
+            for i, lin in enumerate(vl.t.layers):
+                a = a @ lin.weight.t() + lin.bias
+                if i < len(vl.t.layers) - 1:
+                    a = torch.relu(a)
+            z = (mask * z + (1 - mask) * (z + a)).flip(1)
+        if (version == 1 and L % 2 == 0) or (version == 2 and L % 2 == 1):
+            z = z.flip(1)
+    assert (z - y_ref).abs().max().item() <= 1e-12
