@@ -207,25 +207,39 @@ __global__ __launch_bounds__(256, PAIR ? 3 : 4) void k_wgemm(GemmArgs ga) {
     const int n = n0 + c * 32 + r;
     bias_c[c] = (EPI == kEpiBias || EPI == kEpiBiasRelu) && n < N ? j.bias[n] : 0.f;
   }
+  // The epilogue through buffer operations on descriptors based at the
+  // panel's first row: a lane's offset (row 4h, its column) is fixed, each of
+  // its 16 rows adds a wave-uniform scalar offset, and rows past M fall
+  // outside the descriptor's range (loads read 0, stores are dropped) -- no
+  // per-element vector address arithmetic or row guard.  The epilogue's
+  // operands (relu' source h, or the C being added to) are all loaded before
+  // the first store: j.mask / j.C may alias the output as far as the compiler
+  // knows, so loads interleaved with the stores would each pay a full memory
+  // round trip.
+  auto rsrc_rows = [&](const float* base, int64_t ld, int64_t m0) {
+    return __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(base + m0 * ld), 0,
+        (int)std::min<int64_t>((M - m0) * ld * 4, 0x7fffffff), 0x00020000);
+  };
   auto epilogue = [&](const f16v (&acc)[4], int64_t m0) {
-    // the epilogue's operands (relu' source h, or the C being added to) are
-    // all loaded before the first store: j.mask / j.C may alias the output as
-    // far as the compiler knows, so loads interleaved with the stores would
-    // each pay a full memory round trip
     float pre[NC][16];
     if constexpr (EPI == kEpiMask || EPI == kEpiAdd) {
+      const int64_t lds = EPI == kEpiMask ? j.ldm : j.ldc;
+      const auto prs = rsrc_rows(EPI == kEpiMask ? j.mask : j.C, lds, m0);
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
         const int n = n0 + c * 32 + r;
+        const bool ok = EPI == kEpiMask ? n < N : n < j.ldw;
+        const int voff = (4 * h * (int)lds + n) * 4;
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
-          const int64_t m = m0 + (q & 3) + 8 * (q >> 2) + 4 * h;
-          const bool ok = m < M && (EPI == kEpiMask ? n < N : n < j.ldw);
-          pre[c][q] = 0.f;
-          if (ok) pre[c][q] = EPI == kEpiMask ? j.mask[m * j.ldm + n] : j.C[m * j.ldc + n];
+          const float v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+              prs, voff, ((q & 3) + 8 * (q >> 2)) * (int)lds * 4, 0));
+          pre[c][q] = ok ? v : 0.f;
         }
       }
     }
+    const auto crs = rsrc_rows(j.C, j.ldc, m0);
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       const int n = n0 + c * 32 + r;
@@ -233,10 +247,9 @@ __global__ __launch_bounds__(256, PAIR ? 3 : 4) void k_wgemm(GemmArgs ga) {
       const bool real = n < N;
       const float pad = (j.ones && n == N) ? 1.f : 0.f;
       const float b = bias_c[c];
+      const int voff = (4 * h * (int)j.ldc + n) * 4;
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
-        const int64_t m = m0 + (q & 3) + 8 * (q >> 2) + 4 * h;
-        if (m >= M) continue;
         float v = acc[c][q];
         if constexpr (EPI == kEpiBias || EPI == kEpiBiasRelu) v += b;
         if constexpr (EPI == kEpiBiasRelu) {  // the hidden activation
@@ -244,12 +257,13 @@ __global__ __launch_bounds__(256, PAIR ? 3 : 4) void k_wgemm(GemmArgs ga) {
           else v = v < 0.f ? 0.f : v;  // keeps NaN (torch relu)
         }
         if constexpr (EPI == kEpiMask) {  // its derivative from the stored output h
-          const float h = pre[c][q];
-          v = j.act == 2 ? v * (1.f - h * h) : (h > 0.f ? v : 0.f);
+          const float hh = pre[c][q];
+          v = j.act == 2 ? v * (1.f - hh * hh) : (hh > 0.f ? v : 0.f);
           if (!real) v = 0.f;
         }
         if constexpr (EPI == kEpiAdd) v += pre[c][q];
-        j.C[m * j.ldc + n] = real ? v : pad;
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, real ? v : pad), crs, voff,
+                                              ((q & 3) + 8 * (q >> 2)) * (int)j.ldc * 4, 0);
       }
     }
   };
