@@ -764,8 +764,10 @@ int sgpr_run(const Shape& s, const void* prepared, const float* in, float* out, 
                      inverse ? inv_q : fwd_q, flags, log_priors, a);
   // the block-order sum of the loss records: a one-block follow-up launch.
   // (A last-block hand-off inside k_sgpr -- agent-scope fence + counter per
-  // block -- measured 67.6 vs 35.6 us per 2^20-row call: each block's release
-  // fence writes back its XCD's whole L2.)
+  // block -- measured 67.6 vs 35.6 us per 2^20-row call while z was written
+  // through L2: each block's release fence writes back its XCD's L2.  With
+  // the streaming z stores it ties (32.4 vs 32.3 us) and would add a
+  // zeroed-workspace contract, so the follow-up launch stays.)
   if (mode == kLoss) reduce_partials(loss_ws + 4, (int)nblk, 4, 0, nullptr, loss_terms, st);
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) {
