@@ -319,7 +319,7 @@ struct DwArgs {
 
 constexpr int kDwCT = 4;  // column tiles per wave (128 columns)
 
-__global__ __launch_bounds__(256, 2) void k_wdw(DwArgs da) {
+__global__ __launch_bounds__(256, 3) void k_wdw(DwArgs da) {
   // the job's fields once, into scalar registers (a reference into the
   // argument block indexed by blockIdx.y reloads every field at every use)
   const DwJob j = da.job[blockIdx.y];
@@ -344,58 +344,61 @@ __global__ __launch_bounds__(256, 2) void k_wdw(DwArgs da) {
   int hoff[kDwCT];
 #pragma unroll
   for (int c = 0; c < kDwCT; ++c) hoff[c] = (h * ldh + min(c0 + 32 * c + i, ldh - 1)) * 4;
-  auto load = [&](int64_t mr, float (&a)[16], float (&b)[kDwCT][16]) {
+  // 16-row chunks (8 MFMA k-steps) in two operand sets used in turn: the next
+  // chunk's loads are issued before this chunk's MFMAs without register copies
+  constexpr int KS = 8;
+  auto load = [&](int64_t mr, float (&a)[KS], float (&b)[kDwCT][KS]) {
     const auto gr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(j.G + mr * ldg), 0,
                                                       0x7fffffff, 0x00020000);
     const auto hr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(j.H + mr * ldh), 0,
                                                       0x7fffffff, 0x00020000);
 #pragma unroll
-    for (int s = 0; s < 16; ++s)
+    for (int s = 0; s < KS; ++s)
       a[s] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(gr, goff, 2 * s * ldg * 4, 0));
 #pragma unroll
     for (int c = 0; c < kDwCT; ++c)
       if (c < nct) {
 #pragma unroll
-        for (int s = 0; s < 16; ++s)
+        for (int s = 0; s < KS; ++s)
           b[c][s] = __builtin_bit_cast(
               float, __builtin_amdgcn_raw_buffer_load_b32(hr, hoff[c], 2 * s * ldh * 4, 0));
       }
   };
-  auto mfmas = [&](f16v (&acc)[kDwCT], const float (&a)[16], const float (&b)[kDwCT][16]) {
+  auto mfmas = [&](f16v (&acc)[kDwCT], const float* a, const float (*b)[KS], int ks) {
 #pragma unroll
     for (int c = 0; c < kDwCT; ++c)
       if (c < nct) {
 #pragma unroll
-        for (int s = 0; s < 16; ++s)
+        for (int s = 0; s < ks; ++s)
           acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[c][s], acc[c], 0, 0, 0);
       }
   };
   f16v acc[kDwCT];
 #pragma unroll
   for (int c = 0; c < kDwCT; ++c) acc[c] = f16v{};
-  const int64_t rfull = r0 + (r1 - r0) / 32 * 32;  // rows in whole chunks
+  const int64_t rfull = r0 + (r1 - r0) / 16 * 16;  // rows in whole chunks
   if (rfull > r0) {
-    float a[16], b[kDwCT][16];
-    load(r0, a, b);
-    for (int64_t mr = r0; mr < rfull; mr += 32) {
-      float an[16], bn[kDwCT][16];
-      load(mr + 32 < rfull ? mr + 32 : mr, an, bn);
-      __builtin_amdgcn_sched_barrier(0);  // next chunk's loads stay ahead of the MFMAs
-      mfmas(acc, a, b);
-#pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        a[s] = an[s];
-#pragma unroll
-        for (int c = 0; c < kDwCT; ++c) b[c][s] = bn[c][s];
-      }
+    float a0[KS], b0[kDwCT][KS], a1[KS], b1[kDwCT][KS];
+    load(r0, a0, b0);
+    for (int64_t mr = r0;; mr += 32) {
+      const bool more1 = mr + 16 < rfull;
+      if (more1) load(mr + 16, a1, b1);
+      __builtin_amdgcn_sched_barrier(0);
+      mfmas(acc, a0, b0, KS);
+      if (!more1) break;
+      const bool more2 = mr + 32 < rfull;
+      if (more2) load(mr + 32, a0, b0);
+      __builtin_amdgcn_sched_barrier(0);
+      mfmas(acc, a1, b1, KS);
+      if (!more2) break;
     }
   }
   if (rfull < r1) {  // the batch's ragged end: rows past r1 contribute zero
-    float a[16], b[kDwCT][16];
+    float a[KS], b[kDwCT][KS];
     const float* G = j.G;
     const float* H = j.H;
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
+    for (int s = 0; s < KS; ++s) {
       const int64_t row = rfull + 2 * s + h;
       const bool ok = row < r1;
       const int64_t rr = ok ? row : r1 - 1;
@@ -403,7 +406,7 @@ __global__ __launch_bounds__(256, 2) void k_wdw(DwArgs da) {
 #pragma unroll
       for (int c = 0; c < kDwCT; ++c) b[c][s] = H[rr * ldh + min(c0 + 32 * c + i, ldh - 1)];
     }
-    mfmas(acc, a, b);
+    mfmas(acc, a, b, KS);
   }
   float* out = da.partials + (int64_t)blockIdx.x * da.PS;
 #pragma unroll
