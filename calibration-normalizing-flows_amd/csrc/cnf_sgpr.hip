@@ -95,10 +95,19 @@ constexpr int kWaves = 4;  // waves per block
 //      tile's LDS-DMA is issued after the staged tile has been read back;
 //   2  staged through a second LDS tile per wave, stores deferred one tile,
 //      the next tile's DMA issued before the compute (twice the LDS).
+// (A fourth form -- the next tile's DMA issued right after this tile's rows
+// reach registers, outputs staged through a half-size buffer so five waves
+// still fit -- measured 1.5 us SLOWER per 2^20-row loss call and no faster at
+// 2^23: the wave's DMA wait is not what limits the kernel, VALU issue is.)
 #ifndef CNF_SGPR_STAGE
 #define CNF_SGPR_STAGE 1
 #endif
 constexpr int kStage = CNF_SGPR_STAGE;
+// Loss mode picks z[y] from the staged output tile (one LDS read per row);
+// A/B builds: -DCNF_SGPR_NO_GATHER=1 keeps the register select tree.
+#ifndef CNF_SGPR_NO_GATHER
+#define CNF_SGPR_NO_GATHER 0
+#endif
 
 
 
@@ -282,27 +291,42 @@ __device__ __forceinline__ void sp_step(f2 (&v)[P][D], f2 (&ld)[P], SW<SP<D, H1,
 // Loss terms of one pair's rows (logical order):
 // CAL: loss = -(log(softmax(z)[y] + 1e-7) + ld)    calibrators.py:288-291
 // CE:  loss = -log_softmax(z)[y] - det * ld         run_experiment3D.py:107
-template <int D>
+// z[y]: GATHER 1 reads it from the staged output tile (the lane's two rows at
+// tile[0..D) and tile[D..2D): one ds_read_b32 per row instead of a
+// ~30-instruction select tree); GATHER 2 takes the two values gathered by the
+// caller (tile[0], tile[1]); GATHER 0 selects from the registers (ragged tile).
+template <int D, int GATHER>
 __device__ __forceinline__ void pair_loss(const f2* v, f2 ld, uint32_t lab2, int rows, int kind,
-                                          float det, float& t0, float& t1, float& t2) {
+                                          float det, float& t0, float& t1, float& t2,
+                                          const float* tile) {
   const uint32_t b0 = lab2 & 0xffu, b1 = (lab2 >> 8) & 0xffu;
   const bool ok[2] = {b0 != 0xffu, b1 != 0xffu};
   constexpr float kL2E = 1.4426950408889634f, kLN2 = 0.6931471805599453f;
+  float zy[2];
+  if constexpr (GATHER == 1) {  // issued first: the LDS reads overlap the max / sum-exp below
+    zy[0] = tile[ok[0] ? (int)b0 : 0];
+    zy[1] = tile[D + (ok[1] ? (int)b1 : 0)];
+  } else if constexpr (GATHER == 2) {  // gathered by the caller (kStage 3)
+    zy[0] = tile[0];
+    zy[1] = tile[1];
+  }
   f2 m = v[0];
 #pragma unroll
   for (int j = 1; j < D; ++j) m = maxT(m, v[j]);
   const f2 nm = m * splat(-kL2E, f2{});
-  f2 se = splat(0.f, f2{});
+  f2 se = exp2T(fmaT(kL2E, v[0], nm));
 #pragma unroll
-  for (int j = 0; j < D; ++j) se += exp2T(fmaT(kL2E, v[j], nm));
-  uint32_t za[D], zb[D];
+  for (int j = 1; j < D; ++j) se += exp2T(fmaT(kL2E, v[j], nm));
+  if constexpr (GATHER == 0) {
+    uint32_t za[D], zb[D];
 #pragma unroll
-  for (int j = 0; j < D; ++j) {
-    za[j] = __float_as_uint(v[j].x);
-    zb[j] = __float_as_uint(v[j].y);
+    for (int j = 0; j < D; ++j) {
+      za[j] = __float_as_uint(v[j].x);
+      zb[j] = __float_as_uint(v[j].y);
+    }
+    zy[0] = __uint_as_float(sel_tree<D>(za, ok[0] ? (int)b0 : 0, 0));
+    zy[1] = __uint_as_float(sel_tree<D>(zb, ok[1] ? (int)b1 : 0, 0));
   }
-  const float zy[2] = {__uint_as_float(sel_tree<D>(za, ok[0] ? (int)b0 : 0, 0)),
-                       __uint_as_float(sel_tree<D>(zb, ok[1] ? (int)b1 : 0, 0))};
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     if (q >= rows) continue;
@@ -482,12 +506,15 @@ __global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) v
       if constexpr (MODE == kPredict) pair_predict<D>(v[p], lp);
     }
   };
-  auto loss = [&](const f2 (&v)[P][D], const f2 (&ld)[P], uint32_t lab, int nr) {
+  // tile: the lane's staged output rows in LDS (full tiles), or nullptr
+  auto loss = [&](const f2 (&v)[P][D], const f2 (&ld)[P], uint32_t lab, int nr,
+                  const float* tile, auto gather) {
 #pragma unroll
     for (int p = 0; p < P; ++p) {
       const int r = nr - 2 * p;
-      pair_loss<D>(v[p], ld[p], lab >> (16 * p), r < 0 ? 0 : (r > 2 ? 2 : r), a.kind, a.det, lt0,
-                   lt1, lt2);
+      constexpr int G = decltype(gather)::value;
+      pair_loss<D, G>(v[p], ld[p], lab >> (16 * p), r < 0 ? 0 : (r > 2 ? 2 : r), a.kind, a.det,
+                      lt0, lt1, lt2, tile + (G == 2 ? 2 : 2 * D) * p);
     }
   };
 
@@ -521,8 +548,12 @@ __global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) v
 #endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA has landed
     f2 v[P][D];
-    read_pairs<D, P>(sm, lane, v);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // rows are in registers
+    if constexpr (P == 1) {
+      read_pairs_wait<D>(sm, lane, v);  // rows are in registers
+    } else {
+      read_pairs<D, P>(sm, lane, v);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
 #ifdef CNF_SGPR_TRACE
     if (ntr < 2) CNF_TR(1 + 2 * ntr);
 #endif
@@ -540,7 +571,15 @@ __global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) v
     if constexpr (MODE == kLoss) lab = load_labels<D, P>(a.y + row0 + 2 * P * lane, 2 * P, y16);
     f2 ld[P];
     compute(v, ld, row0, 2 * P);
-    if constexpr (MODE == kLoss) loss(v, ld, lab, 2 * P);
+    if constexpr (MODE == kLoss) {
+      if constexpr (kStage == 1 && !CNF_SGPR_NO_GATHER) {
+        // staged first: the loss reads z[y] back from the tile
+        stage_pairs<D, P>(sm, lane, v);
+        loss(v, ld, lab, 2 * P, sm + 2 * P * D * lane, std::integral_constant<int, 1>{});
+      } else {
+        loss(v, ld, lab, 2 * P, sm, std::integral_constant<int, 0>{});
+      }
+    }
 #ifdef CNF_SGPR_TRACE
     if (ntr < 2) CNF_TR(2 + 2 * ntr);
     CNF_TR(5);
@@ -550,7 +589,7 @@ __global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) v
       // stage in the input tile (its rows are in registers), store lane-linear,
       // then let the next tile's DMA in once the staged reads have completed
       if (a.out) {
-        stage_pairs<D, P>(sm, lane, v);
+        if (MODE != kLoss || CNF_SGPR_NO_GATHER) stage_pairs<D, P>(sm, lane, v);
         store_tile<TF>(a.out + row0 * D, sm, lane);
       }
       if (a.ld) store_lds<P>(a.ld + row0 + 2 * P * lane, ld, 2 * P, al_ld);
@@ -596,7 +635,7 @@ __global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) v
     if constexpr (MODE == kLoss) lab = load_labels<D, P>(a.y + r, nr, false);
     f2 ld[P];
     compute(v, ld, row0, nr);
-    if constexpr (MODE == kLoss) loss(v, ld, lab, nr);
+    if constexpr (MODE == kLoss) loss(v, ld, lab, nr, sm, std::integral_constant<int, 0>{});
     if (a.out) store_rows<D, P>(a.out + r * D, v, nr, 4);
     if (a.ld) store_lds<P>(a.ld + r, ld, nr, 4);
   }

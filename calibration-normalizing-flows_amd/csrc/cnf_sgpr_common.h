@@ -152,6 +152,27 @@ __device__ __forceinline__ void read_pairs(const float* sm, int lane, f2 (&v)[P]
     for (int k = 0; k < D; ++k) v[p][k] = f2{b[2 * p * D + k], b[(2 * p + 1) * D + k]};
 }
 
+// read_pairs with the ds_read2_b32 issued as asm straight into the pair
+// registers, then ONE wait that carries every pair as an in/out operand, so
+// no use of a row can be scheduled above it.  (The compiler merged the plain
+// loads into ds_read_b128 of four features of one row, and regrouping those
+// into pairs cost ~15 v_mov per tile.)
+template <int D>
+__device__ __forceinline__ void read_pairs_wait(const float* sm, int lane, f2 (&v)[1][D]) {
+  static_assert(2 * D <= 256, "ds_read2_b32 dword offsets are 8-bit");
+  typedef __attribute__((address_space(3))) const float lds_f;
+  const uint32_t base = (uint32_t)(uintptr_t)(lds_f*)(sm + 2 * D * lane);
+#pragma unroll
+  for (int k = 0; k < D; ++k)
+    asm volatile("ds_read2_b32 %0, %1 offset0:%2 offset1:%3"
+                 : "=v"(v[0][k])
+                 : "v"(base), "i"(k), "i"(D + k)
+                 : "memory");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int k = 0; k < D; ++k) asm volatile("" : "+v"(v[0][k]));
+}
+
 // Coalesced tile stores.  A lane's 2P output rows sit 2*P*D floats apart from
 // the next lane's, so storing them straight from registers makes every 16-B
 // store instruction touch 64 scattered pieces of ~40 cache lines (partial-line
@@ -159,16 +180,26 @@ __device__ __forceinline__ void read_pairs(const float* sm, int lane, f2 (&v)[P]
 // pass).  Instead the lane writes its rows into the wave's LDS tile (row-major,
 // the input tile's layout) and the wave stores the tile lane-linear: each
 // global_store_dwordx4 then writes 1 KiB contiguous (8 whole lines).
+// One ds_write2_b32 per feature and pair writes the pair's two halves
+// straight into their rows (the mirror of read_pairs' ds_read2_b32); plain
+// stores were merged into ds_write_b128 of four features of one row, which
+// costs a v_mov per float to regroup the pair registers.  LDS operations of a
+// wave complete in issue order, so the tile reads that follow need no wait;
+// the "memory" clobber keeps the compiler from moving them above the writes.
 template <int D, int P>
 __device__ __forceinline__ void stage_pairs(float* sm, int lane, const f2 (&v)[P][D]) {
-  float* b = sm + 2 * P * D * lane;
+  static_assert(2 * P * D <= 256, "ds_write2_b32 dword offsets are 8-bit");
+  typedef __attribute__((address_space(3))) float lds_f;
+  const uint32_t base = (uint32_t)(uintptr_t)(lds_f*)(sm + 2 * P * D * lane);
 #pragma unroll
   for (int p = 0; p < P; ++p)
 #pragma unroll
-    for (int k = 0; k < D; ++k) {
-      b[2 * p * D + k] = v[p][k].x;
-      b[(2 * p + 1) * D + k] = v[p][k].y;
-    }
+    for (int k = 0; k < D; ++k)
+      asm volatile("ds_write2_b32 %0, %1, %2 offset0:%3 offset1:%4"
+                   :
+                   : "v"(base), "v"(v[p][k].x), "v"(v[p][k].y), "i"(2 * p * D + k),
+                     "i"((2 * p + 1) * D + k)
+                   : "memory");
 }
 template <int TF>
 __device__ __forceinline__ void store_tile(float* __restrict__ dst, const float* sm, int lane) {
