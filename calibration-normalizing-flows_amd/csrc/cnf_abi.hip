@@ -60,9 +60,9 @@ int derive_shape(const cnf_desc* d, Shape* s) {
     }
   }
   if (s->alt_mask && s->any_perm) return CNF_ERR_DESC;
-  // legacy semantics: the MFMA-tile family only (ReLU / flip-only kernels elsewhere)
-  const bool legacy = s->alt_mask || s->s_tanh;
-  s->valu_id = s->D <= 16 && !legacy ? valu_supported(*s) : -1;
+  // legacy semantics: k_valu (its tables' shapes, forward / inverse / eval) and
+  // the MFMA-tile family; their reverse modes run layer at a time (cnf_wvjp)
+  s->valu_id = s->D <= 16 ? valu_supported(*s) : -1;
   if (s->valu_id >= 0) {
     s->family = Family::kValu;
     int64_t off = 0;

@@ -754,7 +754,8 @@ bool io_ok(const void* p, int64_t align) {
 // Linear fits 32 floats, and the row batch in HBM is 16-B aligned (the LDS-DMA
 // reads whole 16-B words; misaligned views stay on k_valu).
 bool sgpr_enabled(const Shape& s) {
-  return s.sp_ok && !s.strict && s.shift && find(s) && !(s.options & CNF_OPT_NO_SGPR);
+  return s.sp_ok && !s.strict && s.shift && !s.alt_mask && !s.s_tanh && find(s) &&
+         !(s.options & CNF_OPT_NO_SGPR);
 }
 
 int64_t sgpr_blocks(const Shape& s, int64_t B) {

@@ -307,9 +307,9 @@ __global__ void k_prepare(PrepBatch a, float* __restrict__ wreg) {
       float v = 0.f;
       if (i < nW) {
         const int o = (int)(i / S), k = (int)(i - (int64_t)o * S);
-        if (k < g.nin) v = g.W[(int64_t)o * g.nin_full + g.in_off + k];
+        if (k < g.nin) v = g.W[(int64_t)orow(o) * g.nin_full + icol(g.in_off + k)];
       } else if (i - nW < g.nout_full) {
-        v = g.b[i - nW];
+        v = g.b[orow((int)(i - nW))];
       }
       dst[i] = v;
     }
@@ -431,7 +431,7 @@ int prepare_run(const Shape& s, const float* const* params, void* prepared, hipS
         g.nin_full = (int16_t)s.units[i];
         g.rev_in = g.rev_out = 0;
         g.wmul = g.bmul = 1.f;
-        if (tiled && s.alt_mask && (l & 1)) {
+        if (s.alt_mask && (l & 1)) {
           g.rev_in = i == 0;
           g.rev_out = i == s.n_lin - 1;
         }

@@ -41,14 +41,21 @@ using namespace valu;
 // vectors per tile.  PERSIST: a grid of (CUs x resident blocks) walks the
 // tiles, prefetching the next tile's input into registers (16-B loads) while
 // the current tile computes.
+//
+// Legacy alternate mask (alt, CNF_OPT_ALT_MASK; cnf_prepare reverses the odd
+// layers' first-Linear columns and last-Linear rows): the flip-based stack then
+// holds flip^(l+1) of the legacy layer-l output in logical order, i.e. the
+// legacy output in RAW register order -- forward outputs are stored unflipped,
+// and an inverse of an odd-L stack reads its input reversed (its every-layer
+// outputs stay reversed).  SACT: the s-net's hidden activation (2: tanh).
 template <int D, int H1, int H2, bool INV, bool STRICT, int RW, int ROWS, bool PERSIST, int WPE,
-          bool FX, bool WL, bool WU = false, bool CH = false, bool DUP = false>
+          bool FX, bool WL, bool WU = false, bool CH = false, bool DUP = false, int SACT = 1>
 __global__ __launch_bounds__(ROWS, WPE) void k_valu(
     const float* __restrict__ Wg, const int32_t* __restrict__ qtab,
     const int32_t* __restrict__ lflag, const float* __restrict__ in, float* __restrict__ out,
     float* __restrict__ ld_out, float* __restrict__ all, int64_t B, int L, int scale, int shift,
     int any_perm, int vec_io, const int64_t* __restrict__ yl, float* __restrict__ loss_part,
-    int kind, float det, unsigned*, float*) {
+    int kind, float det, int alt) {
   using T = typename RowT<RW>::type;
   constexpr int TR = ROWS * RW;  // rows per tile
   constexpr int TF = TR * D;     // floats per tile
@@ -145,8 +152,21 @@ __global__ __launch_bounds__(ROWS, WPE) void k_valu(
     }
     // rows past the batch end read stale LDS: harmless, never stored
     T v[D];
+    if (INV && alt && (L & 1)) {
 #pragma unroll
-    for (int k = 0; k < D; ++k) v[k] = get_row<ROWS>(sm, tid, D, k, T{});
+      for (int k = 0; k < D; ++k) v[k] = get_row<ROWS>(sm, tid, D, D - 1 - k, T{});
+    } else {
+#pragma unroll
+      for (int k = 0; k < D; ++k) v[k] = get_row<ROWS>(sm, tid, D, k, T{});
+    }
+    // every-layer store in orientation O (alt: the fixed raw orientation)
+    auto st_all = [&](int i, auto O_) {
+      constexpr bool O = decltype(O_)::value;
+      float* dst = all + (int64_t)i * B * D + row0 * D;
+      if (!alt) store_rows<D, ROWS, O>(dst, sm, v, nrows, vec);
+      else if (INV && (L & 1)) store_rows<D, ROWS, true>(dst, sm, v, nrows, vec);
+      else store_rows<D, ROWS, false>(dst, sm, v, nrows, vec);
+    };
 
     T ld = splat(0.f, T{});
     // step index i = 0..L-1; layer = i (forward) or L-1-i (inverse)
@@ -155,29 +175,31 @@ __global__ __launch_bounds__(ROWS, WPE) void k_valu(
     for (; i + 1 < L; i += 2) {
       int la = layer_of(i), lb = layer_of(i + 1);
       bool pa = any_perm && (lflag[la] & kFlagPerm), pb = any_perm && (lflag[lb] & kFlagPerm);
-      step<D, H1, H2, INV, STRICT, false, FX && !STRICT, CH && !WL>(v, ld, WW + (int64_t)la * layer_floats, scale, shift,
-                                          NF, pa, qtab + la * D);
-      if (all) store_rows<D, ROWS, true>(all + (int64_t)i * B * D + row0 * D, sm, v, nrows, vec);
-      step<D, H1, H2, INV, STRICT, true, FX && !STRICT, CH && !WL>(v, ld, WW + (int64_t)lb * layer_floats, scale, shift,
-                                         NF, pb, qtab + lb * D);
-      if (all)
-        store_rows<D, ROWS, false>(all + (int64_t)(i + 1) * B * D + row0 * D, sm, v, nrows, vec);
+      step<D, H1, H2, INV, STRICT, false, FX && !STRICT, CH && !WL, SACT>(
+          v, ld, WW + (int64_t)la * layer_floats, scale, shift, NF, pa, qtab + la * D);
+      if (all) st_all(i, std::true_type{});
+      step<D, H1, H2, INV, STRICT, true, FX && !STRICT, CH && !WL, SACT>(
+          v, ld, WW + (int64_t)lb * layer_floats, scale, shift, NF, pb, qtab + lb * D);
+      if (all) st_all(i + 1, std::false_type{});
     }
     bool odd = i < L;
     if (odd) {
       int la = layer_of(i);
       bool pa = any_perm && (lflag[la] & kFlagPerm);
-      step<D, H1, H2, INV, STRICT, false, FX && !STRICT, CH && !WL>(v, ld, WW + (int64_t)la * layer_floats, scale, shift,
-                                          NF, pa, qtab + la * D);
-      if (all) store_rows<D, ROWS, true>(all + (int64_t)i * B * D + row0 * D, sm, v, nrows, vec);
+      step<D, H1, H2, INV, STRICT, false, FX && !STRICT, CH && !WL, SACT>(
+          v, ld, WW + (int64_t)la * layer_floats, scale, shift, NF, pa, qtab + la * D);
+      if (all) st_all(i, std::true_type{});
     }
+    // final orientation: odd L leaves the row reversed; the alt-mask forward
+    // output is the raw register order
+    const bool orev = odd && !(alt && !INV);
     if (out) {
-      if (odd) store_rows<D, ROWS, true>(out + row0 * D, sm, v, nrows, vec);
+      if (orev) store_rows<D, ROWS, true>(out + row0 * D, sm, v, nrows, vec);
       else store_rows<D, ROWS, false>(out + row0 * D, sm, v, nrows, vec);
     }
     if (ld_out) store_ld<ROWS>(ld_out, row0, tid, nrows, ld);
     if (loss_part) {
-      if (odd) tile_loss<D, true>(v, ld, yv, kind, det, lt0, lt1, lt2);
+      if (orev) tile_loss<D, true>(v, ld, yv, kind, det, lt0, lt1, lt2);
       else tile_loss<D, false>(v, ld, yv, kind, det, lt0, lt1, lt2);
     }
   }
@@ -189,19 +211,21 @@ __global__ __launch_bounds__(ROWS, WPE) void k_valu(
 // ---------------------------------------------------------------------------
 using KFn = void (*)(const float*, const int32_t*, const int32_t*, const float*, float*, float*,
                      float*, int64_t, int, int, int, int, int, const int64_t*, float*, int, float,
-                     unsigned*, float*);
+                     int);
 
 struct Variant {
   KFn fn[2][2];  // [inverse][strict]
   int rw, rows, persist, wl;  // wl: 0 scalar weights, 1 LDS, 2 LDS pairs (DUP)
 };
 
-#define CNF_VARIANT_Y(D, H1, H2, RW, ROWS, P, WPE, FX, WL, WU, CH, DUP)                        \
-  {{{k_valu<D, H1, H2, false, false, RW, ROWS, P, WPE, FX, WL, WU, CH, DUP>,                    \
-     k_valu<D, H1, H2, false, true, RW, ROWS, P, WPE, FX, WL, WU, CH, DUP>},                    \
-    {k_valu<D, H1, H2, true, false, RW, ROWS, P, WPE, FX, WL, WU, CH, DUP>,                     \
-     k_valu<D, H1, H2, true, true, RW, ROWS, P, WPE, FX, WL, WU, CH, DUP>}},                    \
+#define CNF_VARIANT_S(D, H1, H2, RW, ROWS, P, WPE, FX, WL, WU, CH, DUP, SA)                    \
+  {{{k_valu<D, H1, H2, false, false, RW, ROWS, P, WPE, FX, WL, WU, CH, DUP, SA>,                \
+     k_valu<D, H1, H2, false, true, RW, ROWS, P, WPE, FX, WL, WU, CH, DUP, SA>},                \
+    {k_valu<D, H1, H2, true, false, RW, ROWS, P, WPE, FX, WL, WU, CH, DUP, SA>,                 \
+     k_valu<D, H1, H2, true, true, RW, ROWS, P, WPE, FX, WL, WU, CH, DUP, SA>}},                \
    RW, ROWS, P, (WL) ? ((DUP) ? 2 : 1) : 0}
+#define CNF_VARIANT_Y(D, H1, H2, RW, ROWS, P, WPE, FX, WL, WU, CH, DUP) \
+  CNF_VARIANT_S(D, H1, H2, RW, ROWS, P, WPE, FX, WL, WU, CH, DUP, 1)
 #define CNF_VARIANT_X(D, H1, H2, RW, ROWS, P, WPE, FX, WL, WU, CH) \
   CNF_VARIANT_Y(D, H1, H2, RW, ROWS, P, WPE, FX, WL, WU, CH, false)
 #define CNF_VARIANT_U(D, H1, H2, RW, ROWS, P, WPE, FX, WL, WU) \
@@ -240,6 +264,23 @@ const Entry kTable[] = {
     CNF_VALU(10, 7, 0), CNF_VALU(10, 5, 0), CNF_VALU(3, 5, 0),
 };
 
+// Legacy tanh s-net shapes (CNF_OPT_S_TANH; code-old/realNVP.py:61 with its
+// default hidden_size = [dim], and the reference default [5,5]): the same
+// shipped configuration with the s-net's hidden layers on tanhf.
+#define CNF_VALU_TANH(D, H1, H2)                                                          \
+  {D, H1, H2, CNF_VARIANT_S(D, H1, H2, 2, 256, false, 4, true, true, false, false, false, 2), \
+   CNF_VARIANT_S(D, H1, H2, 1, 256, false, 6, true, false, false, false, false, 2),            \
+   Net<D, H1, H2>::floats}
+
+const Entry kLTable[] = {
+    CNF_VALU_TANH(3, 3, 0), CNF_VALU_TANH(10, 10, 0), CNF_VALU_TANH(10, 5, 5),
+};
+constexpr int kLBase = 1000;  // valu_id of kLTable[i] is kLBase + i
+
+const Entry& entry_of(const Shape& s) {
+  return s.valu_id >= kLBase ? kLTable[s.valu_id - kLBase] : kTable[s.valu_id];
+}
+
 int cu_count() {
   static int n = [] {
     int dev = 0, v = 0;
@@ -270,13 +311,18 @@ int valu_supported(const Shape& s) {
   int h1 = s.n_lin >= 2 ? s.units[1] : 0;
   int h2 = s.n_lin >= 3 ? s.units[2] : 0;
   if (s.n_lin > 3) return -1;
+  if (s.s_tanh && s.scale) {
+    for (int i = 0; i < (int)(sizeof(kLTable) / sizeof(kLTable[0])); ++i)
+      if (kLTable[i].D == s.D && kLTable[i].H1 == h1 && kLTable[i].H2 == h2) return kLBase + i;
+    return -1;
+  }
   for (int i = 0; i < (int)(sizeof(kTable) / sizeof(kTable[0])); ++i)
     if (kTable[i].D == s.D && kTable[i].H1 == h1 && kTable[i].H2 == h2) return i;
   return -1;
 }
 
 static const Variant* pick_variant(const Shape& s, int64_t B) {
-  const Entry& e = kTable[s.valu_id];
+  const Entry& e = entry_of(s);
   const bool lds_fits =
       (size_t)256 * 2 * s.D * 4 + (size_t)s.L * s.nets * s.valu_net_floats * 4 <= 64 * 1024;
   return (B > kLargeBatch || !lds_fits) ? &e.large : &e.small;
@@ -317,7 +363,7 @@ int valu_run(const Shape& s, const void* prepared, const float* in, float* out, 
                            loss_terms);
     if (r != CNF_ERR_UNSUPPORTED) return r;
   }
-  const Entry& e = kTable[s.valu_id];
+  const Entry& e = entry_of(s);
   if (e.nf != s.valu_net_floats) return CNF_ERR_DESC;  // host/device layout disagree
   const Variant* var = pick_variant(s, B);
   const char* base = static_cast<const char*>(prepared);
@@ -337,7 +383,7 @@ int valu_run(const Shape& s, const void* prepared, const float* in, float* out, 
   hipLaunchKernelGGL(fn, dim3((unsigned)nblk), dim3(var->rows), lds, st, W,
                      inverse ? inv_q : fwd_q, flags, in, out, ld, all, B, s.L, s.scale, s.shift,
                      s.any_perm ? 1 : 0, vec, y, loss_ws ? loss_ws + 4 : nullptr, kind, det,
-                     nullptr, nullptr);
+                     s.alt_mask ? 1 : 0);
   if (loss_ws) reduce_partials(loss_ws + 4, (int)nblk, 4, 0, nullptr, loss_terms, st);
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) {

@@ -74,6 +74,22 @@ __device__ __forceinline__ V relu(V a) {
   return r;
 }
 
+// Hidden activation of a conditioner Linear: ACT 0 none, 1 ReLU, 2 tanh (the
+// legacy s-net, code-old/realNVP.py:61, CNF_OPT_S_TANH).
+template <int ACT, bool STRICT>
+__device__ __forceinline__ float act(float a) {
+  if constexpr (ACT == 1) return relu<STRICT>(a);
+  else if constexpr (ACT == 2) return tanhf(a);
+  else return a;
+}
+template <int ACT, bool STRICT, class V>
+__device__ __forceinline__ V act(V a) {
+  V r;
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(V) / sizeof(float)); ++i) r[i] = act<ACT, STRICT>(a[i]);
+  return r;
+}
+
 // Compact weight layout of the narrow-flow kernels (written by cnf_prepare):
 // per Linear, W[NOUT][pad4(NIN)] row-major (zero padded), then b[pad4(NOUT)];
 // the first Linear keeps only the NIN = D - D//2 conditioning columns (the
@@ -113,8 +129,8 @@ struct Net {
                                                 Lin<H2, D>::floats;
 };
 
-// y[o] = b[o] (+p0) + sum_k W[o][k] * x[k],  o < NOUT <= NOUTF.
-template <int NIN, int NOUTF, int NOUT, bool RELU, bool STRICT, bool POISON, class T, class WP>
+// y[o] = act(b[o] (+p0) + sum_k W[o][k] * x[k]),  o < NOUT <= NOUTF.
+template <int NIN, int NOUTF, int NOUT, int ACT, bool STRICT, bool POISON, class T, class WP>
 __device__ __forceinline__ void linear(const WP* __restrict__ w, const T* x, T* y, T p0) {
   constexpr int S = Lin<NIN, NOUTF>::stride;
 #pragma unroll
@@ -125,7 +141,7 @@ __device__ __forceinline__ void linear(const WP* __restrict__ w, const T* x, T* 
     for (int k = 0; k < NIN; ++k) {
       a = fmaT(wld(w, o * S + k), x[k], a);
     }
-    y[o] = RELU ? relu<STRICT>(a) : a;
+    y[o] = act<ACT, STRICT>(a);
   }
 }
 
@@ -159,7 +175,7 @@ __device__ __forceinline__ Chunks<NCH> sload(const float* p) {
   return r;
 }
 
-template <int NIN, int NOUTF, int NOUT, bool RELU, bool STRICT, bool POISON, class T>
+template <int NIN, int NOUTF, int NOUT, int ACT, bool STRICT, bool POISON, class T>
 __device__ __forceinline__ void linear_chunked(const float* __restrict__ w, const T* x, T* y,
                                                T p0) {
   constexpr int S = Lin<NIN, NOUTF>::stride;
@@ -170,37 +186,38 @@ __device__ __forceinline__ void linear_chunked(const float* __restrict__ w, cons
     if constexpr (POISON) a += p0;
 #pragma unroll
     for (int k = 0; k < NIN; ++k) a = fmaT(wc[o * S + k], x[k], a);
-    y[o] = RELU ? relu<STRICT>(a) : a;
+    y[o] = act<ACT, STRICT>(a);
   }
 }
 
 // Linear through the chunked scalar path when the block fits 3 chunks.
-template <int NIN, int NOUTF, int NOUT, bool RELU, bool STRICT, bool POISON, bool CH, class T,
+template <int NIN, int NOUTF, int NOUT, int ACT, bool STRICT, bool POISON, bool CH, class T,
           class WP>
 __device__ __forceinline__ void linear_any(const WP* __restrict__ w, const T* x, T* y, T p0) {
   if constexpr (CH && sizeof(WP) == 4 && Lin<NIN, NOUTF>::floats <= 48)
-    linear_chunked<NIN, NOUTF, NOUT, RELU, STRICT, POISON>(w, x, y, p0);
+    linear_chunked<NIN, NOUTF, NOUT, ACT, STRICT, POISON>(w, x, y, p0);
   else
-    linear<NIN, NOUTF, NOUT, RELU, STRICT, POISON>(w, x, y, p0);
+    linear<NIN, NOUTF, NOUT, ACT, STRICT, POISON>(w, x, y, p0);
 }
 
-// Conditioner MLP on the conditioning half c[DC].
-template <int D, int H1, int H2, int NO, bool STRICT, bool CH = false, class T, class WP>
+// Conditioner MLP on the conditioning half c[DC]; HACT: hidden activation.
+template <int D, int H1, int H2, int NO, bool STRICT, bool CH = false, int HACT = 1, class T,
+          class WP>
 __device__ __forceinline__ void mlp(const WP* __restrict__ w, const T* c, T p0, T* o) {
   constexpr int DC = D - D / 2;
   const T z = splat(0.f, T{});
   if constexpr (H1 == 0) {
-    linear_any<DC, D, NO, false, STRICT, STRICT, CH>(w, c, o, p0);
+    linear_any<DC, D, NO, 0, STRICT, STRICT, CH>(w, c, o, p0);
   } else if constexpr (H2 == 0) {
     T h1[H1];
-    linear_any<DC, H1, H1, true, STRICT, STRICT, CH>(w, c, h1, p0);
-    linear_any<H1, D, NO, false, STRICT, false, CH>(w + Lin<DC, H1>::floats, h1, o, z);
+    linear_any<DC, H1, H1, HACT, STRICT, STRICT, CH>(w, c, h1, p0);
+    linear_any<H1, D, NO, 0, STRICT, false, CH>(w + Lin<DC, H1>::floats, h1, o, z);
   } else {
     T h1[H1], h2[H2];
-    linear_any<DC, H1, H1, true, STRICT, STRICT, CH>(w, c, h1, p0);
+    linear_any<DC, H1, H1, HACT, STRICT, STRICT, CH>(w, c, h1, p0);
     const WP* w2 = w + Lin<DC, H1>::floats;
-    linear_any<H1, H2, H2, true, STRICT, false, CH>(w2, h1, h2, z);
-    linear_any<H2, D, NO, false, STRICT, false, CH>(w2 + Lin<H1, H2>::floats, h2, o, z);
+    linear_any<H1, H2, H2, HACT, STRICT, false, CH>(w2, h1, h2, z);
+    linear_any<H2, D, NO, 0, STRICT, false, CH>(w2 + Lin<H1, H2>::floats, h2, o, z);
   }
 }
 
@@ -238,8 +255,9 @@ __device__ __forceinline__ void permute(T* v, const int32_t* __restrict__ q) {
 }
 
 // One coupling layer, input in orientation O, output in orientation !O.
-template <int D, int H1, int H2, bool INV, bool STRICT, bool O, bool FX, bool CH, class T,
-          class WP>
+// SACT: the s-net's hidden activation (1 ReLU; 2 tanh, legacy CNF_OPT_S_TANH).
+template <int D, int H1, int H2, bool INV, bool STRICT, bool O, bool FX, bool CH, int SACT = 1,
+          class T, class WP>
 __device__ __forceinline__ void step(T* v, T& ld, const WP* __restrict__ wl, int scale,
                                      int shift, int net_floats, bool perm,
                                      const int32_t* __restrict__ q) {
@@ -262,7 +280,7 @@ __device__ __forceinline__ void step(T* v, T& ld, const WP* __restrict__ wl, int
   }
   T s[NO], t[NO];
   if (scale) {
-    mlp<D, H1, H2, NO, STRICT, CH>(wl, c, p0, s);
+    mlp<D, H1, H2, NO, STRICT, CH, SACT>(wl, c, p0, s);
     wl += net_floats;
   } else {
 #pragma unroll

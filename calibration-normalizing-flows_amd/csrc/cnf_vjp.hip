@@ -70,15 +70,15 @@ __device__ __forceinline__ void mlp_keep(const float* __restrict__ w, const floa
                                          float* h2, float* out) {
   constexpr int DT = D / 2, DC = D - D / 2;
   if constexpr (H1 == 0) {
-    linear<DC, D, DT, false, false, false>(w, c, out, 0.f);
+    linear<DC, D, DT, 0, false, false>(w, c, out, 0.f);
   } else if constexpr (H2 == 0) {
-    linear<DC, H1, H1, true, false, false>(w, c, h1, 0.f);
-    linear<H1, D, DT, false, false, false>(w + Lin<DC, H1>::floats, h1, out, 0.f);
+    linear<DC, H1, H1, 1, false, false>(w, c, h1, 0.f);
+    linear<H1, D, DT, 0, false, false>(w + Lin<DC, H1>::floats, h1, out, 0.f);
   } else {
-    linear<DC, H1, H1, true, false, false>(w, c, h1, 0.f);
+    linear<DC, H1, H1, 1, false, false>(w, c, h1, 0.f);
     const float* w2 = w + Lin<DC, H1>::floats;
-    linear<H1, H2, H2, true, false, false>(w2, h1, h2, 0.f);
-    linear<H2, D, DT, false, false, false>(w2 + Lin<H1, H2>::floats, h2, out, 0.f);
+    linear<H1, H2, H2, 1, false, false>(w2, h1, h2, 0.f);
+    linear<H2, D, DT, 0, false, false>(w2 + Lin<H1, H2>::floats, h2, out, 0.f);
   }
 }
 
@@ -436,10 +436,13 @@ __global__ __launch_bounds__(kVRows) void k_vjp(
 // [y*R, min(nblk, (y+1)*R)) of columns [64x, 64x + 64) -- four row groups of
 // 64 lanes, four loads in flight each -- and writes the sums to out + y*ostride
 // (ostride = R*PS: in place over the chunk's first row, which only this block
-// reads).  grid.y = 1 gives the final sums.  Fixed grouping: deterministic.
+// reads).  grid.y = 1 gives the final sums; columns from `split` on then go to
+// out2 (the loss sums that follow the gradients in each record), so one pass
+// serves both.  Fixed grouping: deterministic.
 __global__ __launch_bounds__(256) void k_reduce_cols(const float* __restrict__ partials, int nblk,
                                                      int PS, int NE, float* __restrict__ out,
-                                                     int R, int64_t ostride) {
+                                                     int R, int64_t ostride,
+                                                     float* __restrict__ out2, int split) {
   __shared__ float red[256];
   const int e = blockIdx.x * 64 + (threadIdx.x & 63), g = threadIdx.x >> 6;
   const int r0 = (int)blockIdx.y * R, n = min(R, nblk - r0);
@@ -460,10 +463,12 @@ __global__ __launch_bounds__(256) void k_reduce_cols(const float* __restrict__ p
   }
   red[threadIdx.x] = s;
   __syncthreads();
-  if (g == 0 && e < NE)
-    out[(int64_t)blockIdx.y * ostride + e] =
-        ((red[threadIdx.x] + red[threadIdx.x + 64]) + red[threadIdx.x + 128]) +
-        red[threadIdx.x + 192];
+  if (g == 0 && e < NE) {
+    const float v = ((red[threadIdx.x] + red[threadIdx.x + 64]) + red[threadIdx.x + 128]) +
+                    red[threadIdx.x + 192];
+    if (e >= split) out2[e - split] = v;
+    else out[(int64_t)blockIdx.y * ostride + e] = v;
+  }
 }
 
 // The 3 loss sums: ONE wave.  Lane l adds blocks l, l+64, ... in order (eight
@@ -540,7 +545,7 @@ const VEntry kVTable[] = {
 };
 
 const VEntry* find_entry(const Shape& s) {
-  if (s.family != Family::kValu || s.strict) return nullptr;
+  if (s.family != Family::kValu || s.strict || s.alt_mask || s.s_tanh) return nullptr;
   const int h1 = s.n_lin >= 2 ? s.units[1] : 0, h2 = s.n_lin >= 3 ? s.units[2] : 0;
   for (const auto& e : kVTable)
     if (e.D == s.D && e.H1 == h1 && e.H2 == h2) return &e;
@@ -564,7 +569,8 @@ using v2::kV2LMax;
 using v2::kV2SS;
 
 const V2Entry* find_v2(const Shape& s) {
-  if (s.family != Family::kValu || s.strict || !s.sp_ok || !s.shift || s.L > kV2LMax)
+  if (s.family != Family::kValu || s.strict || !s.sp_ok || !s.shift || s.L > kV2LMax ||
+      s.alt_mask || s.s_tanh)
     return nullptr;
   const int h1 = s.n_lin >= 2 ? s.units[1] : 0, h2 = s.n_lin >= 3 ? s.units[2] : 0;
   const V2Entry* parts[3] = {kV2PartA, kV2PartB, kV2PartC};
@@ -617,20 +623,23 @@ int reduce_partials(const float* partials, int nblk, int PS, int P, float* grads
   if (P > 0) {
     // many records: a first pass folds chunks of R records into each chunk's
     // first record (in place), so enough blocks share the read; then the
-    // chunk sums are added in order
-    const unsigned cols = (unsigned)((P + 63) / 64);
+    // chunk sums are added in order.  The loss sums (columns P..P+2 of each
+    // record, when asked for) ride the same passes.
+    const int NE = terms ? P + 3 : P;
+    const unsigned cols = (unsigned)((NE + 63) / 64);
     int nrec = nblk, stride = PS;
     if (nblk >= 128) {
       const int S = std::min(64, nblk / 32), R = (nblk + S - 1) / S;
       const int S2 = (nblk + R - 1) / R;
       float* part = const_cast<float*>(partials);
       hipLaunchKernelGGL(k_reduce_cols, dim3(cols, (unsigned)S2), dim3(256), 0, st, partials, nblk,
-                         PS, P, part, R, (int64_t)R * PS);
+                         PS, NE, part, R, (int64_t)R * PS, (float*)nullptr, NE);
       nrec = S2;
       stride = R * PS;
     }
-    hipLaunchKernelGGL(k_reduce_cols, dim3(cols, 1), dim3(256), 0, st, partials, nrec, stride, P,
-                       grads, nrec, (int64_t)0);
+    hipLaunchKernelGGL(k_reduce_cols, dim3(cols, 1), dim3(256), 0, st, partials, nrec, stride, NE,
+                       grads, nrec, (int64_t)0, terms, P);
+    return CNF_OK;
   }
   const bool r4 = PS == 4 && P == 0 && (reinterpret_cast<uintptr_t>(partials) & 15) == 0;
   if (terms && r4)

@@ -115,6 +115,16 @@ __device__ __forceinline__ void vlin(const SW<NC>& w, const f2* x, f2* y) {
   for (int o = 0; o < NOUT; ++o) y[o] = RELU ? maxT(a[o], splat(0.f, f2{})) : a[o];
 }
 
+// gacc[k] += sum_o W[o][k] gout[o] (the first Linear's input gradient goes
+// straight into the running d/dc of the layer: no separate sum and add)
+template <int NIN, int NOUT, int S, int NC>
+__device__ __forceinline__ void vlin_t_acc(const SW<NC>& w, const f2* gout, f2* gacc) {
+#pragma unroll
+  for (int o = 0; o < NOUT; ++o)
+#pragma unroll
+    for (int k = 0; k < NIN; ++k) gacc[k] = fma_ws(w, widx<S>(o, k), gout[o], gacc[k]);
+}
+
 // gin[k] = sum_o W[o][k] gout[o], k < NIN, o < NOUT
 template <int NIN, int NOUT, int S, int NC>
 __device__ __forceinline__ void vlin_t(const SW<NC>& w, const f2* gout, f2* gin) {
@@ -155,10 +165,66 @@ __device__ __forceinline__ void vnet_fwd(const float* wn, const f2* c, f2* h1, f
   }
 }
 
+// The same net on the SCALED packed region (cnf_sgpr.hip's layout: hidden
+// Linears x 2^-64 with the next Linear's input columns x 2^64, the s-net's last
+// Linear x log2 e): ReLU is the clamp bit of each hidden neuron's last FMA, so
+// h1, h2 come out as h' = 2^-64 h (exact: powers of two) and the s-net's output
+// as s' = log2(e) s.  Saves the two unpacked v_max (plus their canonicalising
+// copies) per pair and hidden neuron of the plain form.
+template <int NIN, int NOUT, int S, bool CLAMP, int NC>
+__device__ __forceinline__ void vlin_sp(const SW<NC>& w, const f2* x, f2* y) {
+  f2 a[NOUT];
+#pragma unroll
+  for (int o = 0; o < NOUT; ++o)
+    a[o] = (CLAMP && NIN == 1) ? fma_wb_clamp(w.pair(o * S), x[0]) : fma_wb(w.pair(o * S), x[0]);
+#pragma unroll
+  for (int k = 1; k < NIN; ++k)
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o)
+      a[o] = (CLAMP && k == NIN - 1) ? fma_ws_clamp(w, widx<S>(o, k), x[k], a[o])
+                                     : fma_ws(w, widx<S>(o, k), x[k], a[o]);
+#pragma unroll
+  for (int o = 0; o < NOUT; ++o) y[o] = a[o];
+}
+template <class S, int NC>
+__device__ __forceinline__ void vnet_fwd_sp(const float* wn, const f2* c, f2* h1, f2* h2, f2* out) {
+  SW<NC> A, Bw;
+  sissue(A, wn);
+  if constexpr (S::NL == 1) {
+    sready();
+    vlin_sp<S::nin(0), S::nout(0), S::stride(0), false>(A, c, out);
+  } else if constexpr (S::NL == 2) {
+    sready();
+    sissue(Bw, wn + S::off(1));
+    vlin_sp<S::nin(0), S::nout(0), S::stride(0), true>(A, c, h1);
+    sready();
+    vlin_sp<S::nin(1), S::nout(1), S::stride(1), false>(Bw, h1, out);
+  } else {
+    sready();
+    sissue(Bw, wn + S::off(1));
+    vlin_sp<S::nin(0), S::nout(0), S::stride(0), true>(A, c, h1);
+    sready();
+    sissue(A, wn + S::off(2));
+    vlin_sp<S::nin(1), S::nout(1), S::stride(1), true>(Bw, h1, h2);
+    sready();
+    vlin_sp<S::nin(2), S::nout(2), S::stride(2), false>(A, h2, out);
+  }
+}
+
 // relu' from the stored activation h (>= 0, or NaN): keeps g where h > 0
+#ifndef CNF_V2_CLAMP_MASK
 __device__ __forceinline__ f2 relu_mask(f2 g, f2 h) {
   return f2{h.x > 0.f ? g.x : 0.f, h.y > 0.f ? g.y : 0.f};
 }
+#else
+// A/B: the mask as clamp(h' 2^127) (packed; NaN clamps to 0) times g -- exact
+// for h' = 2^-64 h >= 2^-127, i.e. every pre-activation above 2^-63
+__device__ __forceinline__ f2 relu_mask(f2 g, f2 h) {
+  f2 m;
+  asm("v_pk_mul_f32 %0, %1, %2 clamp" : "=v"(m) : "v"(h), "s"(splat(0x1p127f, f2{})));
+  return g * m;
+}
+#endif
 
 // Back-propagate one net: gout (d/d out) -> adds d/dc into gc and leaves the
 // gradient stack G = [g_a1, g_a2, gout] (pre-activation gradients).
@@ -168,11 +234,10 @@ __device__ __forceinline__ void vnet_bwd(const float* wn, const f2* h1, const f2
   constexpr int H1 = S::NL >= 2 ? S::nout(0) : 0, H2 = S::NL == 3 ? S::nout(1) : 0;
   constexpr int DT = S::DT, DC = S::DC;
   SW<NC> A, Bw;
-  f2 gin[DC];
   if constexpr (S::NL == 1) {
     sissue(A, wn);
     sready();
-    vlin_t<DC, DT, S::stride(0)>(A, gout, gin);
+    vlin_t_acc<DC, DT, S::stride(0)>(A, gout, gc);
   } else if constexpr (S::NL == 2) {
     f2 g1[H1];
     sissue(A, wn + S::off(1));
@@ -182,7 +247,7 @@ __device__ __forceinline__ void vnet_bwd(const float* wn, const f2* h1, const f2
 #pragma unroll
     for (int m = 0; m < H1; ++m) G[m] = g1[m] = relu_mask(g1[m], h1[m]);
     sready();
-    vlin_t<DC, H1, S::stride(0)>(Bw, g1, gin);
+    vlin_t_acc<DC, H1, S::stride(0)>(Bw, g1, gc);
   } else {
     f2 g2[H2], g1[H1];
     sissue(A, wn + S::off(2));
@@ -197,12 +262,10 @@ __device__ __forceinline__ void vnet_bwd(const float* wn, const f2* h1, const f2
 #pragma unroll
     for (int m = 0; m < H1; ++m) G[m] = g1[m] = relu_mask(g1[m], h1[m]);
     sready();
-    vlin_t<DC, H1, S::stride(0)>(A, g1, gin);
+    vlin_t_acc<DC, H1, S::stride(0)>(A, g1, gc);
   }
 #pragma unroll
   for (int j = 0; j < DT; ++j) G[H1 + H2 + j] = gout[j];
-#pragma unroll
-  for (int k = 0; k < DC; ++k) gc[k] += gin[k];
 }
 
 // Fold G^T H of this tile's 128 rows (GS x HS <= 16 x 16) into acc: the stage
@@ -321,6 +384,10 @@ __global__ __launch_bounds__(64, 2) void k_vjp2(const float* __restrict__ W,
   const int ntiles = (int)((B + kV2TR - 1) / kV2TR);
   const f2 zero = splat(0.f, f2{});
   constexpr float kLN2 = 0.69314718055994531f, kL2E = 1.4426950408889634f;
+  // the scaled packed region (forward sweep and recompute) sits right before
+  // the plain one (back-propagation): cnf_prepare's sp_region / vp_region
+  const float* __restrict__ Wsp = W - (int64_t)L * LF;
+  constexpr float kTwo64 = 0x1p64f;  // h = 2^64 h' (exact)
   floatx4 acc[kV2LMax][NETS];
 #pragma unroll
   for (int l = 0; l < kV2LMax; ++l)
@@ -377,13 +444,14 @@ __global__ __launch_bounds__(64, 2) void k_vjp2(const float* __restrict__ W,
           }
         }
       }
-      vnet_fwd<S, NC>(wl + (NETS == 2 ? S::NF : 0), c, h1, h2, t);
-      if constexpr (NETS == 2) vnet_fwd<S, NC>(wl, c, h1, h2, sv);
+      const float* ws = Wsp + (int64_t)l * LF;
+      vnet_fwd_sp<S, NC>(ws + (NETS == 2 ? S::NF : 0), c, h1, h2, t);
+      if constexpr (NETS == 2) vnet_fwd_sp<S, NC>(ws, c, h1, h2, sv);  // sv = log2(e) s
 #pragma unroll
       for (int j = 0; j < DT; ++j) {
         f2& x = v[R<D, O>(j)];
         if constexpr (NETS == 2) {
-          x = fmaV(x, exp2T(sv[j] * splat(kL2E, f2{})), t[j]);
+          x = fmaV(x, exp2T(sv[j]), t[j]);
           ld += sv[j];
         } else {
           x += t[j];
@@ -400,6 +468,7 @@ __global__ __launch_bounds__(64, 2) void k_vjp2(const float* __restrict__ W,
     }
     const bool oddL = l < L;
     if (oddL) fwd(std::false_type{}, l);
+    if constexpr (NETS == 2) ld = ld * splat(kLN2, f2{});  // ln2 sum(s')
 
     // ---- upstream gradient at z_L (orientation L & 1) ----
     f2 g[D];
@@ -473,7 +542,7 @@ __global__ __launch_bounds__(64, 2) void k_vjp2(const float* __restrict__ W,
       constexpr int l = decltype(LI)::value;
       constexpr bool Oc = ((l + 1) & 1) != 0;  // orientation of z_l
       constexpr bool Oi = !Oc;
-      if (a.gz_all) {
+      if (!LOSS && a.gz_all) {  // (the loss entry points never pass gz_all)
 #pragma unroll
         for (int j = 0; j < D; ++j)
           g[R<D, Oc>(j)] += f2{nr > 0 ? a.gz_all[((int64_t)l * B + r) * D + j] : 0.f,
@@ -485,7 +554,12 @@ __global__ __launch_bounds__(64, 2) void k_vjp2(const float* __restrict__ W,
           permute<D, Oc>(g, iq + l * D);
         }
       }
-      const float* wl = W + (int64_t)l * LF;
+      // the layer's weight offset laundered through an SGPR: left as a constant,
+      // the compiler hoists all eight layers' 64-bit block addresses out of the
+      // tile loop and spills them to VGPR lanes (v_readlane before every load)
+      int lofs = l * LF;
+      asm volatile("" : "+s"(lofs));
+      const float* wl = W + lofs;
       f2 c[DC], gT[DT], gc[DC];
 #pragma unroll
       for (int k = 0; k < DC; ++k) {
@@ -506,8 +580,11 @@ __global__ __launch_bounds__(64, 2) void k_vjp2(const float* __restrict__ W,
             xT[j] = f2{nr > 0 ? sp[2 * j] : 0.f, nr > 1 ? sp[2 * j + 1] : 0.f};
         }
       }
+      // recompute on the scaled weights: th / sh are 2^-64 h (relu' reads
+      // their sign; the weight-gradient stack H takes 2^64 times them)
+      const float* ws = Wsp + lofs;
       f2 th1[H1 ? H1 : 1], th2[H2 ? H2 : 1], t[DT];
-      vnet_fwd<S, NC>(wl + (NETS == 2 ? S::NF : 0), c, th1, th2, t);
+      vnet_fwd_sp<S, NC>(ws + (NETS == 2 ? S::NF : 0), c, th1, th2, t);
       f2 H[HS];
 #pragma unroll
       for (int k = 0; k < DC; ++k) H[k] = c[k];
@@ -516,11 +593,11 @@ __global__ __launch_bounds__(64, 2) void k_vjp2(const float* __restrict__ W,
       const f2 keep = f2{nr > 0 ? 1.f : 0.f, nr > 1 ? 1.f : 0.f};
       if constexpr (NETS == 2) {
         f2 sh1[H1 ? H1 : 1], sh2[H2 ? H2 : 1], sv[DT];
-        vnet_fwd<S, NC>(wl, c, sh1, sh2, sv);
+        vnet_fwd_sp<S, NC>(ws, c, sh1, sh2, sv);  // sv = log2(e) s
         f2 gs[DT];
 #pragma unroll
         for (int j = 0; j < DT; ++j) {
-          const f2 e = exp2T(sv[j] * splat(kL2E, f2{}));
+          const f2 e = exp2T(sv[j]);
           gs[j] = fmaV(gT[j] * xT[j], e, gld);  // z_T = x_T e^s + t, ld += s
           gT[j] = gT[j] * e;
         }
@@ -531,9 +608,9 @@ __global__ __launch_bounds__(64, 2) void k_vjp2(const float* __restrict__ W,
           for (int f = 0; f < GS; ++f) G[f] *= keep;
         }
 #pragma unroll
-        for (int m = 0; m < H1; ++m) H[DC + m] = sh1[m];
+        for (int m = 0; m < H1; ++m) H[DC + m] = sh1[m] * splat(kTwo64, f2{});
 #pragma unroll
-        for (int m = 0; m < H2; ++m) H[DC + H1 + m] = sh2[m];
+        for (int m = 0; m < H2; ++m) H[DC + H1 + m] = sh2[m] * splat(kTwo64, f2{});
         acc[l][0] = wgrad_tile<GS, HS>(st, G, H, lane, acc[l][0]);
       }
       {  // t-net: d/dt = g_T (before the e^s scaling of the s-net branch)
@@ -547,9 +624,9 @@ __global__ __launch_bounds__(64, 2) void k_vjp2(const float* __restrict__ W,
           for (int f = 0; f < GS; ++f) G[f] *= keep;
         }
 #pragma unroll
-        for (int m = 0; m < H1; ++m) H[DC + m] = th1[m];
+        for (int m = 0; m < H1; ++m) H[DC + m] = th1[m] * splat(kTwo64, f2{});
 #pragma unroll
-        for (int m = 0; m < H2; ++m) H[DC + H1 + m] = th2[m];
+        for (int m = 0; m < H2; ++m) H[DC + H1 + m] = th2[m] * splat(kTwo64, f2{});
         acc[l][NETS - 1] = wgrad_tile<GS, HS>(st, G, H, lane, acc[l][NETS - 1]);
       }
 #pragma unroll

@@ -1,5 +1,6 @@
 """Legacy semantics (flows/legacy.py, include/cnf.h CNF_OPT_ALT_MASK /
-CNF_OPT_S_TANH) on the native MFMA-tile kernels against the torch
+CNF_OPT_S_TANH) on the native kernels (k_valu for the D <= 16 shapes of its
+tables, the MFMA-tile family otherwise) against the torch
 restatement on the CPU.  Parity UNPINNED against the reference itself
 (code-old/realNVP.py needs TensorFlow, absent): the restatement is the check."""
 import os
@@ -32,9 +33,19 @@ def _rel(a, b):
     return ((a - b).abs() / (b.abs() + 1)).max().item()
 
 
+# legacy shapes k_valu serves (its tables: cnf_valu.hip kTable, and kLTable for
+# the tanh s-net); every other legacy shape stays on the MFMA-tile family
+_NARROW = {(10, (10,)), (10, (5, 5)), (3, (3,))}
+
+
+def _kernel(D, hidden):
+    return "valu-fused" if (D, tuple(hidden)) in _NARROW else "mfma-tile"
+
+
 @pytest.mark.parametrize("D,L,hidden,s_act", [
     (10, 4, [10], "tanh"),      # code-old defaults: hidden [dim], layers 4
     (10, 3, [5, 5], "tanh"),    # odd L: one final un-flip
+    (3, 5, [3], "tanh"),        # odd D and L, hidden [dim] (k_valu tanh table)
     (7, 5, [6], "relu"),        # odd D
     (100, 2, [100, 100], "tanh"),
     (20, 1, [], "tanh"),
@@ -53,7 +64,7 @@ def test_legacy_forward_inverse_and_grads(D, L, hidden, s_act):
     gx_ref = xc.grad.clone()
 
     fg = f.to(DEV)
-    assert fg._native_stack().kernel_name() == "mfma-tile"
+    assert fg._native_stack().kernel_name() == _kernel(D, hidden)
     n0 = engine.stats["forward"] + engine.stats["inverse"]
     with torch.no_grad():
         y, ld = fg(x.to(DEV))
@@ -99,7 +110,7 @@ def test_legacy_nice_v3_native_matches_restatement(D, L, hidden):
     gx_ref = xc.grad.clone()
 
     fg = f.to(DEV)
-    assert fg._native_stack().kernel_name() == "mfma-tile"
+    assert fg._native_stack().kernel_name() == _kernel(D, hidden)
     n0 = engine.stats["forward"] + engine.stats["inverse"]
     with torch.no_grad():
         y, ld = fg(x.to(DEV))
