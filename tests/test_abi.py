@@ -65,6 +65,21 @@ def test_kernel_family_selection():
     assert name(_lib.make_desc(10, 3, [4, 6, 3])) == "mfma-tile"
 
 
+def test_legacy_kernel_family_selection():
+    """Legacy stacks (CNF_OPT_ALT_MASK / S_TANH) of k_valu's shapes run on k_valu
+    (never on k_sgpr), the rest on the MFMA-tile family."""
+    name = lambda d: _lib.lib().cnf_kernel_name(ctypes.byref(d)).decode()
+    alt, tanh = _lib.OPT_ALT_MASK, _lib.OPT_S_TANH
+    assert name(_lib.make_desc(10, 4, [10], options=alt | tanh)) == "valu-fused"
+    assert name(_lib.make_desc(10, 3, [5, 5], options=alt | tanh)) == "valu-fused"
+    assert name(_lib.make_desc(3, 5, [3], options=alt | tanh)) == "valu-fused"
+    assert name(_lib.make_desc(10, 4, [5, 5], options=alt)) == "valu-fused"      # not k_sgpr
+    assert name(_lib.make_desc(10, 4, [10], scale=0, options=alt)) == "valu-fused"  # NICE v3
+    assert name(_lib.make_desc(10, 4, [5, 5], options=tanh)) == "valu-fused"
+    assert name(_lib.make_desc(10, 4, [7], options=alt | tanh)) == "mfma-tile"  # no tanh table
+    assert name(_lib.make_desc(20, 1, [], options=alt | tanh)) == "mfma-tile"
+
+
 @pytest.mark.parametrize("mutate,status", [
     (lambda d: setattr(d, "abi_version", 99), -2),
     (lambda d: setattr(d, "dim", 1), -2),
