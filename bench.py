@@ -116,7 +116,7 @@ class Runner:
     """Pre-built C-ABI launches of one fused pass over rotating buffers.
     mode: "forward" (cnf_forward / cnf_inverse), "loss" (cnf_forward_loss)."""
 
-    def __init__(self, w, device, rotate_bytes, all_outputs=False, mode="forward"):
+    def __init__(self, w, device, rotate_bytes, all_outputs=False, mode="forward", data=None):
         from cnf_hip import _lib
         self.w = w
         self.dev = device
@@ -127,10 +127,12 @@ class Runner:
         B, D, L = w["B"], w["D"], w["L"]
         self.mode = mode
         per_set = algo_bytes_per_vec(D, L, all_outputs, mode == "loss") * B
-        self.nsets = max(1, min(64, math.ceil(rotate_bytes / per_set)))
+        # data: one caller-given (x [B, D], y [B]) set instead of rotating
+        # synthetic ones (the sharded-eval test feeds each rank its shard)
+        self.nsets = 1 if data is not None else max(1, min(64, math.ceil(rotate_bytes / per_set)))
         self.sets = []
         for i in range(self.nsets):
-            x, y = synthetic_logits(B, D, device, 1234 + i)
+            x, y = data if data is not None else synthetic_logits(B, D, device, 1234 + i)
             ld = torch.empty(B, device=device)
             if all_outputs:
                 out, allt = None, torch.empty(L, B, D, device=device)
@@ -471,7 +473,11 @@ def main():
                              NllAllReduce(runner, overlap=not args.overlap_allreduce))
         sync_ms = round(ts / args.steps * 1e3, 5)
     t = torch.tensor([t_dev], dtype=torch.float64, device=dev)
+    rank_ms = [round(t_dev / args.steps * 1e3, 5)]
     if world > 1:
+        every = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(every, t)
+        rank_ms = [round(v.item() / args.steps * 1e3, 5) for v in every]
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     t_max = t.item()
     total_vecs = w["B"] * world * args.steps
@@ -532,6 +538,10 @@ def main():
             "unit": "logit-vectors/sec",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(t_max / args.steps * 1e3, 5),
+            # the rank count the process group reports, and each rank's own
+            # ms/step (ms_per_step above is their max)
+            "ranks": dist.get_world_size() if dist.is_initialized() else 1,
+            "rank_ms_per_step": rank_ms,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f32", "data": "synthetic",
             "config": {"workload": "%s: %d-layer %s coupling, D=%d, hidden_size=%s, %d vectors "

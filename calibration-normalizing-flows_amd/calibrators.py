@@ -214,7 +214,10 @@ class TorchFlowCalibrator(Calibrator):
         self.flow.to(self.dev)
         stack = _native_stack(self.flow, self.dev)
         if stack is not None:
-            history = self._fit_native(stack, logits, target, epochs, batch_size)
+            # the captured epochs launch on the CURRENT device's stream: make
+            # that the calibrator's `dev`, which need not be the current GPU
+            with torch.cuda.device(logits.device):
+                history = self._fit_native(stack, logits, target, epochs, batch_size)
         else:
             history = self._fit_torch(logits, target, epochs, batch_size)
         self.flow.cpu()

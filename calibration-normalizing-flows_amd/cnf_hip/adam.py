@@ -18,6 +18,26 @@ from . import _lib
 from .engine import _ptr, _stream, stats
 
 
+def supports(opt):
+    """True when `opt` is an optimizer whose update cnf_adam_step reproduces:
+    exactly torch.optim.Adam (not a subclass such as AdamW, whose decay is
+    decoupled), with amsgrad, maximize and decoupled weight decay off."""
+    if type(opt) is not torch.optim.Adam:
+        return False
+    return not any(g.get("amsgrad") or g.get("maximize") or g.get("decoupled_weight_decay")
+                   for g in opt.param_groups)
+
+
+def group_lr(torch_adam, stack):
+    """The current learning rate of the param group holding the stack's
+    parameters (an LR scheduler may have changed it since the last step)."""
+    ids = {id(p) for p in stack.param_tensors()}
+    for g in torch_adam.param_groups:
+        if any(id(p) in ids for p in g["params"]):
+            return float(g["lr"].item() if torch.is_tensor(g["lr"]) else g["lr"])
+    raise ValueError("StackAdam: the optimizer holds none of the stack's parameters")
+
+
 class StackAdam:
     """Adam state (two flat moment buffers) for one CouplingStack."""
 
@@ -41,9 +61,16 @@ class StackAdam:
         if g.get("amsgrad") or g.get("maximize"):
             raise ValueError("StackAdam: amsgrad / maximize are not supported")
         lr = g["lr"].item() if torch.is_tensor(g["lr"]) else g["lr"]
+        if not supports(torch_adam):
+            raise ValueError("StackAdam: only a plain torch.optim.Adam (coupled weight decay) "
+                             "is supported, got %s" % type(torch_adam).__name__)
         self = cls(stack, lr, g["betas"], g["eps"], g["weight_decay"])
         st = [torch_adam.state.get(p) for p in ps]
-        if all(s is not None and "exp_avg" in s for s in st):
+        have = [s is not None and "exp_avg" in s for s in st]
+        if any(have) and not all(have):
+            raise ValueError("StackAdam: the torch optimizer holds state for some of the "
+                             "stack's parameters but not all (%d of %d)" % (sum(have), len(have)))
+        if all(have):
             steps = {int(s["step"]) for s in st}
             if len(steps) != 1:
                 raise ValueError("StackAdam: parameters at different step counts")

@@ -21,8 +21,13 @@ forward needs the updated weights); overlapping it with the reverse mode
 would need per-layer buckets of the layer-at-a-time wide VJP.  At cfg4
 (727,200 floats = 2.9 MB per step) a ring all-reduce over 8 ranks moves
 2 * 7/8 * 2.9 MB per rank, about 40 us at 7 x 153 GB/s of xGMI even before
-latency terms, against a ~25 ms step: under 0.5 %, so one bucket at the end
-of the step ships.
+latency terms, against a 17-18 ms step (round 3): under 0.3 %, so one bucket
+at the end of the step ships.
+
+The native Adam step (cnf_adam_step) serves exactly torch.optim.Adam; any
+other optimizer (SGD, AdamW, amsgrad) receives the reduced gradient in .grad
+and steps itself.  The learning rate is re-read from the param group at every
+step, so LR schedulers apply.
 
 grad_scale = 1 / global batch, so the summed gradient is exactly the gradient
 of the reference's -mean over the whole (unsharded) batch.  For cfg2
@@ -112,21 +117,39 @@ class ShardedFlowTrainer:
                            grads_out=buf[:P], terms_out=buf[P:])
             if self.world > 1:
                 dist.all_reduce(buf, group=self.group)
+            from .adam import supports, group_lr
+            if not supports(self.optimizer):
+                # any other optimizer (SGD, AdamW, amsgrad ...) steps itself
+                # on the reduced gradient, as on the CPU path
+                self._set_grads(buf[:P])
+                self.optimizer.step()
+                return buf[P:]
             if self._adam is None or self._adam.stack is not stack:
+                if self._adam is not None:
+                    # a rebuilt stack (e.g. after invalidate_native): carry the
+                    # moments and step count over through the torch state
+                    self._adam.store_into(self.optimizer)
                 self._adam = StackAdam.like(stack, self.optimizer)
+            self._adam.lr = group_lr(self.optimizer, stack)  # LR schedulers
             self._adam.step(buf[:P])
             return buf[P:]
         grads, terms = local_loss_and_grads(self.flow, x, y, 1.0 / global_batch, kind, det)
         buf = torch.cat([grads, terms])
         if self.world > 1:
             dist.all_reduce(buf, group=self.group)
+        off = self._set_grads(buf)
+        self.optimizer.step()
+        return buf[off:off + 3]
+
+    def _set_grads(self, flat):
+        """Scatter the flat (reduced) gradient into the parameters' .grad;
+        returns the number of floats consumed."""
         off = 0
         for p in self.params:
             n = p.numel()
-            p.grad = buf[off:off + n].view_as(p).clone()
+            p.grad = flat[off:off + n].view_as(p).clone()
             off += n
-        self.optimizer.step()
-        return buf[off:off + 3]
+        return off
 
     def sync_optimizer(self):
         """Write the native Adam's step count and moments into the torch
@@ -146,6 +169,23 @@ class ShardedFlowTrainer:
         if self.world > 1:
             dist.all_reduce(terms, group=self.group)
         return terms
+
+
+@torch.no_grad()
+def sharded_nll(flow, x, y, group=None, kind=_lib.LOSS_CAL, det=1.0):
+    """configs[2]'s step: this rank's shard through the fused forward + loss
+    (cnf_forward_loss on a ROCm device, the torch path on CPU), then ONE
+    all-reduce of the 3 sums.  Returns the global (loss, ce, ld) sums; divide
+    by the global row count for the reference's means (calibrators.py:297-317)."""
+    stack = _native(flow, x)
+    if stack is not None:
+        terms, _, _ = stack.forward_loss(x, y, kind=kind, det=det)
+    else:
+        _, terms = local_loss_and_grads(flow, x, y, 0.0, kind, det)
+    terms = terms.clone()
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(terms, group=group)
+    return terms
 
 
 def shard(n, rank, world):

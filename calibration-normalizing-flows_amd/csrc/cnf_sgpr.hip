@@ -103,6 +103,13 @@ constexpr int kWaves = 4;  // waves per block
 #define CNF_SGPR_STAGE 1
 #endif
 constexpr int kStage = CNF_SGPR_STAGE;
+// Loss mode: the block-order sum of the per-block loss records by the
+// launch's last block (cnf_valu_io.h block_sum3_handoff) instead of a
+// one-block follow-up launch.
+#ifndef CNF_SGPR_FUSED_RED
+#define CNF_SGPR_FUSED_RED 0
+#endif
+constexpr bool kFusedRed = CNF_SGPR_FUSED_RED != 0;
 // Loss mode picks z[y] from the staged output tile (one LDS read per row);
 // A/B builds: -DCNF_SGPR_NO_GATHER=1 keeps the register select tree.
 #ifndef CNF_SGPR_NO_GATHER
@@ -407,6 +414,8 @@ struct KArgs {
   float* all;             // [L][B][D] every-layer outputs (ALL variants)
   const int64_t* y;       // labels (loss)
   float* part;            // per-block loss partials, 4 floats each (loss)
+  uint32_t* ctr;          // arrival counter of the in-launch block-order sum (loss)
+  float* terms;           // loss_terms[3] (loss, in-launch sum)
   int64_t B;
   int L, kind;
   float det;
@@ -642,7 +651,10 @@ __global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) v
   CNF_TRC(1);
   CNF_TR(6);
   if constexpr (MODE == kLoss) {
-    block_sum3<kWaves * 64>(lt0, lt1, lt2, smem, a.part);
+    if constexpr (kFusedRed)
+      block_sum3_handoff<kWaves * 64>(lt0, lt1, lt2, smem, a.part, a.ctr, (int)gridDim.x, a.terms);
+    else
+      block_sum3<kWaves * 64>(lt0, lt1, lt2, smem, a.part);
   }
 }
 
@@ -795,6 +807,8 @@ int sgpr_run(const Shape& s, const void* prepared, const float* in, float* out, 
   a.all = all;
   a.y = y;
   a.part = loss_ws ? loss_ws + 4 : nullptr;
+  a.ctr = reinterpret_cast<uint32_t*>(loss_ws);
+  a.terms = loss_terms;
   a.B = B;
   a.L = s.L;
   a.kind = kind;
@@ -808,7 +822,10 @@ int sgpr_run(const Shape& s, const void* prepared, const float* in, float* out, 
   // through L2: each block's release fence writes back its XCD's L2.  With
   // the streaming z stores it ties (32.4 vs 32.3 us) and would add a
   // zeroed-workspace contract, so the follow-up launch stays.)
-  if (mode == kLoss) reduce_partials(loss_ws + 4, (int)nblk, 4, 0, nullptr, loss_terms, st);
+#ifndef CNF_AB_NO_REDUCE  // A/B timing only: the loss sums are not formed
+  if (mode == kLoss && !kFusedRed)
+    reduce_partials(loss_ws + 4, (int)nblk, 4, 0, nullptr, loss_terms, st);
+#endif
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) {
     set_hip_error(err);

@@ -209,9 +209,12 @@ __global__ __launch_bounds__(256, PAIR ? 3 : 4) void k_wgemm(GemmArgs ga) {
   }
   // The epilogue through buffer operations on descriptors based at the
   // panel's first row: a lane's offset (row 4h, its column) is fixed, each of
-  // its 16 rows adds a wave-uniform scalar offset, and rows past M fall
-  // outside the descriptor's range (loads read 0, stores are dropped) -- no
-  // per-element vector address arithmetic or row guard.  The epilogue's
+  // its 16 rows adds a wave-uniform scalar offset -- no per-element vector
+  // address arithmetic or row guard on a full panel.  The descriptor's range
+  // check covers only the VGPR offset (+ immediate), never the scalar one, so
+  // the batch's ragged last panel moves each row's offset into the VGPR
+  // operand: its rows past M then fall outside the range (loads read 0,
+  // stores are dropped) instead of landing past the end of C.  The epilogue's
   // operands (relu' source h, or the C being added to) are all loaded before
   // the first store: j.mask / j.C may alias the output as far as the compiler
   // knows, so loads interleaved with the stores would each pay a full memory
@@ -221,7 +224,15 @@ __global__ __launch_bounds__(256, PAIR ? 3 : 4) void k_wgemm(GemmArgs ga) {
         const_cast<float*>(base + m0 * ld), 0,
         (int)std::min<int64_t>((M - m0) * ld * 4, 0x7fffffff), 0x00020000);
   };
+  // byte offsets of row q of a lane's 16 (rows (q & 3) + 8 (q >> 2) past the
+  // lane's 4h) as (VGPR part, scalar part): the scalar part on full panels,
+  // all of it in the VGPR on the ragged one (see above)
+  auto row_off = [](bool full, int voff, int q, int ld) {
+    const int so = ((q & 3) + 8 * (q >> 2)) * ld * 4;
+    return full ? int2{voff, so} : int2{voff + so, 0};
+  };
   auto epilogue = [&](const f16v (&acc)[4], int64_t m0) {
+    const bool full = m0 + 32 <= M;  // wave-uniform
     float pre[NC][16];
     if constexpr (EPI == kEpiMask || EPI == kEpiAdd) {
       const int64_t lds = EPI == kEpiMask ? j.ldm : j.ldc;
@@ -233,8 +244,9 @@ __global__ __launch_bounds__(256, PAIR ? 3 : 4) void k_wgemm(GemmArgs ga) {
         const int voff = (4 * h * (int)lds + n) * 4;
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
+          const int2 o = row_off(full, voff, q, (int)lds);
           const float v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-              prs, voff, ((q & 3) + 8 * (q >> 2)) * (int)lds * 4, 0));
+              prs, o.x, o.y, 0));
           pre[c][q] = ok ? v : 0.f;
         }
       }
@@ -262,8 +274,9 @@ __global__ __launch_bounds__(256, PAIR ? 3 : 4) void k_wgemm(GemmArgs ga) {
           if (!real) v = 0.f;
         }
         if constexpr (EPI == kEpiAdd) v += pre[c][q];
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, real ? v : pad), crs, voff,
-                                              ((q & 3) + 8 * (q >> 2)) * (int)j.ldc * 4, 0);
+        const int2 o = row_off(full, voff, q, (int)j.ldc);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, real ? v : pad), crs, o.x,
+                                              o.y, 0);
       }
     }
   };

@@ -77,3 +77,33 @@ def test_noninvertible_flow_raises():
     f = Flow([PlanarLayer(3), NvpCouplingLayer(3)])
     with pytest.raises(ValueError, match="Flow inverse not tractable!"):
         f.backward(torch.randn(4, 3))
+
+
+def test_stack_adam_refuses_partial_torch_state():
+    """StackAdam.like (cnf_hip/adam.py) resumes from a torch.optim.Adam only
+    when EVERY stack parameter has state; partial state must raise instead of
+    silently restarting all moments at step 0 (advisor finding, round 3)."""
+    import pytest
+    from cnf_hip.adam import StackAdam, supports
+
+    class _Stack:
+        def __init__(self, ps):
+            self.ps = ps
+
+        def param_tensors(self):
+            return self.ps
+
+    ps = [torch.nn.Parameter(torch.randn(3)), torch.nn.Parameter(torch.randn(2))]
+    opt = torch.optim.Adam(ps, lr=1e-3)
+    ps[0].grad = torch.ones(3)
+    opt.step()  # state for ps[0] only
+    with pytest.raises(ValueError, match="some of"):
+        StackAdam.like(_Stack(ps), opt)
+    ps[1].grad = torch.ones(2)
+    ps[0].grad = torch.ones(3)
+    opt.step()
+    with pytest.raises(ValueError, match="different step"):
+        StackAdam.like(_Stack(ps), opt)
+    assert supports(torch.optim.Adam(ps)) and not supports(torch.optim.AdamW(ps))
+    assert not supports(torch.optim.Adam(ps, amsgrad=True))
+    assert not supports(torch.optim.SGD(ps, lr=0.1))

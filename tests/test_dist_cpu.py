@@ -113,3 +113,14 @@ def test_shard_covers_batch_exactly():
             parts = [shard(n, r, w) for r in range(w)]
             assert parts[0][0] == 0 and parts[-1][1] == n
             assert all(parts[i][1] == parts[i + 1][0] for i in range(w - 1))
+
+
+def test_cfg3_sharded_eval_wiring_gloo():
+    """configs[2]'s sharding + NLL all-reduce wiring on CPU (gloo, 2 ranks,
+    the torch path of cnf_hip.dist.sharded_nll): the reduced sums equal one
+    process's eval over both shards, and sampled rows match the oracle.  The
+    same check runs on RCCL over every visible GPU in tests/test_gpu_cfg3.py."""
+    _setup_path()
+    from _cfg3_worker import check_against_single, run_ranks
+    res = run_ranks(2, "gloo", 3000)
+    check_against_single(res, 3000, torch.device("cpu"))

@@ -12,6 +12,7 @@
 #   train        cfg2 / cfg4 fused training-step times (bench.train_step_rate)
 #   wide         cfg4 forward (k_wide) time
 #   calib        the calibrator-fit epoch variant (bench.calibrator_epoch_rate)
+#   abterms      tools/ab/ab_terms.py (loss-term bits + fp64 check) for every tools/ab/lib*.so
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -30,7 +31,7 @@ for step in "$@"; do
     tests) TAILN=12 run tests 600 python -u -m pytest tests -m gpu -q -rfs --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) TAILN=2 run bench 600 python bench.py ;;
-    trace) run trace_loss 180 python tools/sgpr_trace.py loss && run trace_fwd 180 python tools/sgpr_trace.py forward ;;
+    trace) CNF_TRACE_DUMP=gpurun_out/trace_loss.npz run trace_loss 180 python tools/sgpr_trace.py loss && CNF_TRACE_DUMP=gpurun_out/trace_fwd.npz run trace_fwd 180 python tools/sgpr_trace.py forward ;;
     rate) run rate 300 python tools/quick_rate.py loss forward inverse ;;
     train) run train 300 python -c "import json, torch, bench; d = torch.device('cuda:0'); print(json.dumps({w: bench.train_step_rate(d, w, steps=(20 if w == 'cfg2' else 5)) for w in ('cfg2', 'cfg4')}))" ;;
     wide) run wide 300 python -c "import json, torch, bench; d = torch.device('cuda:0'); r = bench.Runner(dict(bench.WORKLOADS['cfg4']), d, 1e9); t = min(bench.kernel_only_seconds(r, 10) for _ in range(3)); print(json.dumps({'cfg4_forward_us': round(t * 1e6, 1)}))" ;;
@@ -40,6 +41,12 @@ for step in "$@"; do
         [ -e "$lib" ] || continue
         n=$(basename "$lib" .so)
         TAILN=${AB_TAIL:-4} CNF_HIP_LIB=$PWD/$lib run "ab_$n" 300 python tools/quick_rate.py ${AB_MODE:-loss}
+      done ;;
+    abterms)
+      for lib in tools/ab/lib*.so; do
+        [ -e "$lib" ] || continue
+        n=$(basename "$lib" .so)
+        CNF_HIP_LIB=$PWD/$lib run "abterms_$n" 300 python tools/ab/ab_terms.py
       done ;;
     prof:*)  # prof:<workload>:<mode>:<launches> -> gpurun_out/prof_<workload>_<mode>/
       IFS=: read -r _ wl md nl <<< "$step"

@@ -104,3 +104,5 @@ blk = gw // 4
 dec = np.minimum((blk * 10) // max(1, blk.max() + 1), 9)
 out["start_us_by_block_decile"] = [round(float(np.median(start[dec == d])), 2) for d in range(10)]
 print(json.dumps(out))
+if os.environ.get("CNF_TRACE_DUMP"):  # raw marks for offline analysis
+    np.savez_compressed(os.environ["CNF_TRACE_DUMP"], marks=raw, clk=clk, B=B)
