@@ -261,8 +261,10 @@ class CouplingStack:
     def predict(self, x, log_priors, want_logdet=False):
         """Calibrated probabilities softmax(log(softmax(flow(x - mean x)) + 1e-7)
         - log_priors) (Calibrator.predict, calibrators.py:40-44, 330-353):
-        one fused cnf_predict launch, or -- for shapes it does not cover --
-        cnf_forward followed by the same math as device torch ops."""
+        one fused cnf_predict launch (k_sgpr, random_flip included; k_wide),
+        or -- for shapes it does not cover (strict_nan, legacy options, wide
+        shapes outside k_wide's table) -- cnf_forward followed by the same
+        math as device torch ops."""
         x = self._check_input(x)
         B = x.shape[0]
         dev = x.device

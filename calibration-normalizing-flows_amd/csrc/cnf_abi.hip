@@ -242,11 +242,15 @@ int cnf_predict(const cnf_desc* desc, const void* prepared, const float* x,
   int st = derive_shape(desc, &s);
   if (st != CNF_OK) return st;
   if (B < 0) return CNF_ERR_BATCH;
-  if (s.family != Family::kValu || !sgpr_enabled(s)) return CNF_ERR_UNSUPPORTED;
+  const bool narrow = s.family == Family::kValu && sgpr_enabled(s);
+  const bool wide = s.family == Family::kTile && s.wide_floats > 0 && wide_ok(s);
+  if (!narrow && !wide) return CNF_ERR_UNSUPPORTED;
   if (B == 0) return CNF_OK;
   if (!prepared || !x || !log_priors || !probs) return CNF_ERR_NULL;
   auto mis = [](const void* p) { return p && (reinterpret_cast<uintptr_t>(p) & 3); };
   if (mis(x) || mis(probs) || mis(logdet) || mis(log_priors)) return CNF_ERR_ALIGN;
+  if (wide)  // k_wide's predict mode (centre + flow + softmax + prior correction)
+    return wide_run(s, prepared, x, probs, logdet, B, false, (hipStream_t)stream, log_priors);
   return sgpr_run(s, prepared, x, probs, logdet, nullptr, B, false, (hipStream_t)stream, nullptr,
                   nullptr, 0, 0.f, nullptr, log_priors);
 }
@@ -291,6 +295,7 @@ int cnf_vjp_inverse_workspace_bytes(const cnf_desc* desc, int64_t B, size_t* byt
   if (st != CNF_OK) return st;
   if (!bytes) return CNF_ERR_NULL;
   if (B < 0) return CNF_ERR_BATCH;
+  if (s.strict) return CNF_ERR_UNSUPPORTED;  // strict: the forward's reverse mode only
   return wvjp_workspace(s, B, bytes);
 }
 

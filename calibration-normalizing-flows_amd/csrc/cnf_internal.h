@@ -101,7 +101,7 @@ int64_t wide_layer_floats(const Shape& s);  // 0 when the shape has no k_wide in
 bool wide_ok(const Shape& s);               // k_wide serves this descriptor's final outputs
 int wide_prepare(const Shape& s, const float* const* params, void* prepared, hipStream_t st);
 int wide_run(const Shape& s, const void* prepared, const float* in, float* out, float* ld,
-             int64_t B, bool inverse, hipStream_t st);
+             int64_t B, bool inverse, hipStream_t st, const float* log_priors = nullptr);
 
 // layer-at-a-time MFMA reverse mode of the tile family (cnf_wvjp.hip)
 bool wvjp_ok(const Shape& s);

@@ -536,7 +536,14 @@ __global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) v
                             __builtin_amdgcn_s_getreg((31 << 11) | 4);  // XCC_ID, HW_ID
   int ntr = 0;
 #endif
-  int t = gw;
+#ifndef CNF_SGPR_PRIO
+#define CNF_SGPR_PRIO 0
+#endif
+  // PRIO 3: the youngest waves own the extra tiles (tile walk from the last wave)
+  const int gwt = CNF_SGPR_PRIO == 3 ? nw - 1 - gw : gw;
+  if (CNF_SGPR_PRIO == 3) left = gwt < ntiles ? (ntiles - 1 - gwt) / nw + 1 : 0;
+  const int owned = left;
+  int t = gwt;
 #ifdef CNF_AB_STAGGER  // A/B: later resident blocks of a CU request their first tile later
   {
     const int slot = (int)(((int64_t)blockIdx.x * CNF_SGPR_GRID_WPS) / gridDim.x);
@@ -550,10 +557,19 @@ __global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) v
   for (; t < nfull; t += nw) {
     --left;  // tiles after this one
 #ifndef CNF_AB_NO_PRIO
-    if (left >= 3) __builtin_amdgcn_s_setprio(3);
-    else if (left == 2) __builtin_amdgcn_s_setprio(2);
-    else if (left == 1) __builtin_amdgcn_s_setprio(1);
-    else __builtin_amdgcn_s_setprio(0);
+    if constexpr (CNF_SGPR_PRIO == 0) {  // longest-remaining first
+      if (left >= 3) __builtin_amdgcn_s_setprio(3);
+      else if (left == 2) __builtin_amdgcn_s_setprio(2);
+      else if (left == 1) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+    } else if constexpr (CNF_SGPR_PRIO == 1) {  // every wave's first tile ahead of later ones
+      if (left + 1 == owned) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+    } else if constexpr (CNF_SGPR_PRIO == 2) {  // tiles with successors, then lone tiles, then last
+      if (left >= 1) __builtin_amdgcn_s_setprio(2);
+      else if (owned == 1) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+    }
 #endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA has landed
     f2 v[P][D];
@@ -667,7 +683,7 @@ struct KV {
 };
 
 // variants without permutation: fwd, inv, loss, predict; with a random_flip
-// permutation: fwd, inv.  The every-layer-output form (ALL) is not
+// permutation: fwd, inv, predict.  The every-layer-output form (ALL) is not
 // instantiated: those launches go to k_valu, whose LDS-staged stores write
 // the L*B*D floats faster (cnf_valu.hip valu_run); ALL stays as a template
 // switch for A/B builds.
@@ -676,7 +692,7 @@ enum Var { vFwd, vInv, vLoss, vPredict, kNVar };
 struct SEntry {
   int D, H1, H2;
   KV fn[2][kNVar];  // [nets - 1][variant]
-  KV pfn[2][2];     // [nets - 1][fwd, inv] with permutation
+  KV pfn[2][3];     // [nets - 1][fwd, inv, predict] with permutation
 };
 
 #define CNF_K(D, H1, H2, N, M, A, P) \
@@ -685,7 +701,8 @@ struct SEntry {
   {CNF_K(D, H1, H2, N, kFwd, false, false), CNF_K(D, H1, H2, N, kInv, false, false),           \
    CNF_K(D, H1, H2, N, kLoss, false, false), CNF_K(D, H1, H2, N, kPredict, false, false)}
 #define CNF_SP(D, H1, H2, N)                                                                  \
-  {CNF_K(D, H1, H2, N, kFwd, false, true), CNF_K(D, H1, H2, N, kInv, false, true)}
+  {CNF_K(D, H1, H2, N, kFwd, false, true), CNF_K(D, H1, H2, N, kInv, false, true),             \
+   CNF_K(D, H1, H2, N, kPredict, false, true)}
 #define CNF_SGPR(D, H1, H2) \
   {D, H1, H2, {CNF_SV(D, H1, H2, 1), CNF_SV(D, H1, H2, 2)}, {CNF_SP(D, H1, H2, 1), CNF_SP(D, H1, H2, 2)}}
 
@@ -742,8 +759,8 @@ const KV* pick(const SEntry* e, const Shape& s, int mode, bool all) {
   const int n = s.scale ? 1 : 0;
   if (all) return nullptr;  // k_valu serves every-layer outputs
   if (s.any_perm) {
-    if (mode == kLoss || mode == kPredict) return nullptr;  // k_valu handles these
-    return &e->pfn[n][mode == kInv ? 1 : 0];
+    if (mode == kLoss) return nullptr;  // k_valu handles the permuted fused eval
+    return &e->pfn[n][mode == kInv ? 1 : (mode == kPredict ? 2 : 0)];
   }
   return &e->fn[n][mode];
 }

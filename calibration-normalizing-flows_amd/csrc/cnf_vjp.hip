@@ -127,7 +127,7 @@ __device__ __forceinline__ void net_backward(const float* __restrict__ w, const 
     float gh1[H1];
     linear_t<H1, D, DT>(w + Lin<DC, H1>::floats, gout, gh1);
 #pragma unroll
-    for (int m = 0; m < H1; ++m) gh1[m] = h1[m] > 0.f ? gh1[m] : 0.f;
+    for (int m = 0; m < H1; ++m) gh1[m] = h1[m] <= 0.f ? 0.f : gh1[m];
     linear_t<DC, H1, H1>(w, gh1, gin);
 #pragma unroll
     for (int m = 0; m < H1; ++m) G[m] = gh1[m];
@@ -143,10 +143,10 @@ __device__ __forceinline__ void net_backward(const float* __restrict__ w, const 
     float gh2[H2], gh1[H1];
     linear_t<H2, D, DT>(w3, gout, gh2);
 #pragma unroll
-    for (int k = 0; k < H2; ++k) gh2[k] = h2[k] > 0.f ? gh2[k] : 0.f;
+    for (int k = 0; k < H2; ++k) gh2[k] = h2[k] <= 0.f ? 0.f : gh2[k];
     linear_t<H1, H2, H2>(w2, gh2, gh1);
 #pragma unroll
-    for (int m = 0; m < H1; ++m) gh1[m] = h1[m] > 0.f ? gh1[m] : 0.f;
+    for (int m = 0; m < H1; ++m) gh1[m] = h1[m] <= 0.f ? 0.f : gh1[m];
     linear_t<DC, H1, H1>(w, gh1, gin);
 #pragma unroll
     for (int m = 0; m < H1; ++m) G[m] = gh1[m];

@@ -211,10 +211,11 @@ __device__ __forceinline__ void vnet_fwd_sp(const float* wn, const f2* c, f2* h1
   }
 }
 
-// relu' from the stored activation h (>= 0, or NaN): keeps g where h > 0
+// relu' from the stored activation h, as torch's threshold_backward: drops g
+// where h <= 0 and keeps it otherwise (a NaN activation passes g through)
 #ifndef CNF_V2_CLAMP_MASK
 __device__ __forceinline__ f2 relu_mask(f2 g, f2 h) {
-  return f2{h.x > 0.f ? g.x : 0.f, h.y > 0.f ? g.y : 0.f};
+  return f2{h.x <= 0.f ? 0.f : g.x, h.y <= 0.f ? 0.f : g.y};
 }
 #else
 // A/B: the mask as clamp(h' 2^127) (packed; NaN clamps to 0) times g -- exact

@@ -243,11 +243,64 @@ __device__ __forceinline__ void relayout(float* st, int* qs, int S, const int32_
   wsync();
 }
 
-template <int D, int H1, int H2, bool INV, int NETS>
+// The calibrator's predict on rows staged in LDS (calibrators.py:40-44,
+// 330-353): two lanes per row (lane l: row l & 31, features of half l >> 5),
+// their partial sums / maxima joined by one cross-half shuffle.
+template <int D>
+__device__ __forceinline__ void row_centre(float* st, int S, int lane) {
+  constexpr int HF = (D + 1) / 2;
+  const int row = lane & 31, f0 = (lane >> 5) * HF, f1 = f0 + HF < D ? f0 + HF : D;
+  float* r = st + row * S;
+  float s = 0.f;
+  for (int f = f0; f < f1; ++f) s += r[f];
+  s += __shfl_xor(s, 32);
+  const float mu = s * (1.f / D);
+  for (int f = f0; f < f1; ++f) r[f] -= mu;
+}
+// softmax(log(softmax(z) + 1e-7) - log_priors), in place
+template <int D>
+__device__ __forceinline__ void row_predict(float* st, int S, int lane,
+                                            const float* __restrict__ lp) {
+  constexpr int HF = (D + 1) / 2;
+  constexpr float kL2E = 1.4426950408889634f, kLN2 = 0.6931471805599453f;
+  const int row = lane & 31, f0 = (lane >> 5) * HF, f1 = f0 + HF < D ? f0 + HF : D;
+  float* r = st + row * S;
+  float m = -__builtin_inff();
+  for (int f = f0; f < f1; ++f) m = fmaxf(m, r[f]);
+  m = fmaxf(m, __shfl_xor(m, 32));
+  float se = 0.f;
+  for (int f = f0; f < f1; ++f) {
+    const float e = __builtin_amdgcn_exp2f((r[f] - m) * kL2E);
+    r[f] = e;
+    se += e;
+  }
+  se += __shfl_xor(se, 32);
+  const float inv = 1.f / se;
+  float m2 = -__builtin_inff();
+  for (int f = f0; f < f1; ++f) {
+    const float a = __builtin_amdgcn_logf(r[f] * inv + 1e-7f) * kLN2 - lp[f];
+    r[f] = a;
+    m2 = fmaxf(m2, a);
+  }
+  m2 = fmaxf(m2, __shfl_xor(m2, 32));
+  float s2 = 0.f;
+  for (int f = f0; f < f1; ++f) {
+    const float e = __builtin_amdgcn_exp2f((r[f] - m2) * kL2E);
+    r[f] = e;
+    s2 += e;
+  }
+  s2 += __shfl_xor(s2, 32);
+  const float inv2 = 1.f / s2;
+  for (int f = f0; f < f1; ++f) r[f] *= inv2;
+}
+
+// PRED: the fused calibrated predict (centre, forward, softmax, prior
+// correction; lpri = log priors [D]), else forward (INV false) / inverse.
+template <int D, int H1, int H2, bool INV, int NETS, bool PRED = false>
 __global__ __launch_bounds__(64 * kWWaves, CNF_WIDE_WPE) void k_wide(
     const float* __restrict__ W, const int32_t* __restrict__ qtab,
     const float* __restrict__ in, float* __restrict__ out, float* __restrict__ ld_out,
-    int64_t B, int L) {
+    int64_t B, int L, const float* __restrict__ lpri) {
   using G = WG<D, H1, H2>;
   constexpr int TX = G::TX, TS = G::TS;
   constexpr int S = D | 1;  // odd LDS row stride: one slot of 32 rows spans 32 banks
@@ -267,6 +320,10 @@ __global__ __launch_bounds__(64 * kWWaves, CNF_WIDE_WPE) void k_wide(
     st[r * S + f] = r < nrows ? src[i] : 0.f;
   }
   wsync();
+  if constexpr (PRED) {  // x - mean(x) per row (calibrators.py:42)
+    row_centre<D>(st, S, lane);
+    wsync();
+  }
   v16 X[TX];
   {
     const int row = lane & 31, h = lane >> 5;
@@ -315,6 +372,10 @@ __global__ __launch_bounds__(64 * kWWaves, CNF_WIDE_WPE) void k_wide(
   // slots -> LDS rows -> coalesced stores
   put_state<D, TX>(st, S, X, lane);
   wsync();
+  if constexpr (PRED) {
+    row_predict<D>(st, S, lane, lpri);
+    wsync();
+  }
   if (out) {
     float* dst = out + row0 * D;
     for (int i = lane; i < nrows * D; i += 64) {
@@ -329,7 +390,8 @@ __global__ __launch_bounds__(64 * kWWaves, CNF_WIDE_WPE) void k_wide(
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
-using WFn = void (*)(const float*, const int32_t*, const float*, float*, float*, int64_t, int);
+using WFn = void (*)(const float*, const int32_t*, const float*, float*, float*, int64_t, int,
+                    const float*);
 
 constexpr int kMaxKs = 1 + (CNF_MAX_WIDTH / 32 + 1) * 16;  // bias + widest input x 16
 
@@ -391,7 +453,7 @@ void fill_segment(int i, WSeg* g) {
 
 struct WEntry {
   int D, H1, H2;
-  WFn fn[2][2];  // [nets - 1][inverse]
+  WFn fn[2][3];  // [nets - 1][forward, inverse, predict]
   int net_floats, lin_off[3], mfmas;
   void (*fill)(int, WSeg*);
 };
@@ -399,8 +461,10 @@ struct WEntry {
 #define CNF_WG(D, H1, H2) WG<D, H1, H2>
 #define CNF_WIDE(D, H1, H2)                                                       \
   {D, H1, H2,                                                                     \
-   {{k_wide<D, H1, H2, false, 1>, k_wide<D, H1, H2, true, 1>},                    \
-    {k_wide<D, H1, H2, false, 2>, k_wide<D, H1, H2, true, 2>}},                   \
+   {{k_wide<D, H1, H2, false, 1>, k_wide<D, H1, H2, true, 1>,                     \
+     k_wide<D, H1, H2, false, 1, true>},                                          \
+    {k_wide<D, H1, H2, false, 2>, k_wide<D, H1, H2, true, 2>,                     \
+     k_wide<D, H1, H2, false, 2, true>}},                                         \
    CNF_WG(D, H1, H2)::NF,                                                         \
    {0, CNF_WG(D, H1, H2)::lin_off(1), CNF_WG(D, H1, H2)::lin_off(2)},             \
    CNF_WG(D, H1, H2)::mfmas(), fill_segment<D, H1, H2>}
@@ -473,7 +537,7 @@ int wide_prepare(const Shape& s, const float* const* params, void* prepared, hip
 }
 
 int wide_run(const Shape& s, const void* prepared, const float* in, float* out, float* ld,
-             int64_t B, bool inverse, hipStream_t st) {
+             int64_t B, bool inverse, hipStream_t st, const float* log_priors) {
   const WEntry* e = wfind(s);
   if (!e) return CNF_ERR_UNSUPPORTED;
   const char* base = static_cast<const char*>(prepared);
@@ -482,9 +546,10 @@ int wide_run(const Shape& s, const void* prepared, const float* in, float* out, 
   const float* W = reinterpret_cast<const float*>(base + idx_bytes(s)) + s.wide_region;
   const int64_t rows_per_block = (int64_t)kWRows * kWWaves;
   const dim3 grid((unsigned)((B + rows_per_block - 1) / rows_per_block)), block(64 * kWWaves);
-  WFn fn = e->fn[s.nets - 1][inverse ? 1 : 0];
+  if (log_priors && inverse) return CNF_ERR_UNSUPPORTED;
+  WFn fn = e->fn[s.nets - 1][log_priors ? 2 : (inverse ? 1 : 0)];
   hipLaunchKernelGGL(fn, grid, block, wide_lds(s), st, W, inverse ? inv_q : fwd_q, in, out, ld, B,
-                     s.L);
+                     s.L, log_priors);
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) {
     set_hip_error(err);

@@ -73,6 +73,8 @@ struct GemmJob {
   int64_t lda, lda2, ldm, ldc;
   int ldb, ldb2, N, K, ldw, ones;
   int act;  // hidden activation of this net: 1 ReLU, 2 tanh (legacy s-net, CNF_OPT_S_TANH)
+  int zlt;  // kEpiAdd: columns n < zlt add 0 * v (strict: the mask's zero columns, where
+            // autograd's grad * mask keeps a NaN / inf gradient as NaN)
 };
 struct GemmArgs {
   GemmJob job[2];  // one per conditioner net (grid.z)
@@ -270,10 +272,10 @@ __global__ __launch_bounds__(256, PAIR ? 3 : 4) void k_wgemm(GemmArgs ga) {
         }
         if constexpr (EPI == kEpiMask) {  // its derivative from the stored output h
           const float hh = pre[c][q];
-          v = j.act == 2 ? v * (1.f - hh * hh) : (hh > 0.f ? v : 0.f);
+          v = j.act == 2 ? v * (1.f - hh * hh) : (hh <= 0.f ? 0.f : v);
           if (!real) v = 0.f;
         }
-        if constexpr (EPI == kEpiAdd) v += pre[c][q];
+        if constexpr (EPI == kEpiAdd) v = (n < j.zlt ? 0.f * v : v) + pre[c][q];
         const int2 o = row_off(full, voff, q, (int)j.ldc);
         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, real ? v : pad), crs, o.x,
                                               o.y, 0);
@@ -448,10 +450,21 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
-// Row geometry of the stash layout (see the file comment).
+// Row geometry of the stash layout (see the file comment).  strict
+// (cnf_desc.strict_nan): the first Linear reads the reference's whole masked
+// input x_b = mask * x (0 * x_T: 0, or NaN where x_T is not finite) and the
+// last Linear writes s, t for all D features, so the C part is
+// [x_b (D) | 1 | pad] and raw x_j sits in the C part for j >= DT (mask 1:
+// x_b = x) and in the T part for j < DT; O rows (and G of the last Linear)
+// are Op = r8(D) wide instead of DTp.
 struct Geo {
-  int D, DT, DC, Cp, DTp, Dp;
-  __device__ __forceinline__ int col(int i) const { return i < DT ? Cp + i : i - DT; }
+  int D, DT, DC, Cp, DTp, Dp, Op, strict;
+  // column of RAW x_j in a stash row
+  __device__ __forceinline__ int col(int i) const {
+    return i < DT ? Cp + i : (strict ? i : i - DT);
+  }
+  // the C part's ones column
+  __device__ __forceinline__ int ones() const { return strict ? D : DC; }
 };
 
 // A layer's gather table (D <= CNF_MAX_DIM ints) staged in LDS once per block:
@@ -473,8 +486,9 @@ __global__ __launch_bounds__(256) void k_wstash(const float* __restrict__ x,
   for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < B; r += nw) {
     for (int c = lane; c < g.Dp; c += 64) {
       float v;
-      if (c < g.DC) v = x[r * g.D + g.DT + c];
-      else if (c == g.DC) v = 1.f;
+      if (g.strict && c < g.D) v = c < g.DT ? 0.f * x[r * g.D + c] : x[r * g.D + c];  // mask * x
+      else if (!g.strict && c < g.DC) v = x[r * g.D + g.DT + c];
+      else if (c == g.ones()) v = 1.f;
       else if (c >= g.Cp && c < g.Cp + g.DT) v = x[r * g.D + c - g.Cp];
       else v = 0.f;
       xs[r * g.Dp + c] = v;
@@ -485,6 +499,9 @@ __global__ __launch_bounds__(256) void k_wstash(const float* __restrict__ x,
 // Coupling update of one layer (flows/flows.py:101-112), one wave per row:
 //   z_i = x_i e^{s_i} + t_i (i < DT), x_i otherwise; ld += sum_i s_i;
 //   out[j] = z[fq[j]] (permutation, then flip); stash layout in and out.
+// strict: the reference's own op sequence over ALL features,
+//   z_i = m_i x_i + (1 - m_i) (x_i e^{s_i} + t_i),  ld += sum_i (1 - m_i) s_i,
+// one rounding per op, so 0 * inf = NaN at masked positions as in torch.
 // A wave takes kRU rows at a time and issues every load of the group before
 // the first use (lane l: columns j = l + 64q), so a wave has kRU rows of
 // loads in flight instead of one row's dependent round trips.
@@ -517,12 +534,12 @@ __global__ __launch_bounds__(256) void k_wfwd_update(const float* __restrict__ X
         v[u][q] = sv[u][q] = tv[u][q] = so[u][q] = 0.f;
         if (j < g.D) {
           v[u][q] = X[r * g.Dp + g.col(i)];
-          if (i < g.DT) {
-            if (Os) sv[u][q] = Os[r * g.DTp + i];
-            if (Ot) tv[u][q] = Ot[r * g.DTp + i];
+          if (i < g.DT || g.strict) {
+            if (Os) sv[u][q] = Os[r * g.Op + i];
+            if (Ot) tv[u][q] = Ot[r * g.Op + i];
           }
         }
-        if (Os && j < g.DT) so[u][q] = Os[r * g.DTp + j];
+        if (Os && j < (g.strict ? g.D : g.DT)) so[u][q] = Os[r * g.Op + j];
       }
     }
 #pragma unroll
@@ -536,12 +553,19 @@ __global__ __launch_bounds__(256) void k_wfwd_update(const float* __restrict__ X
         const int j = lane + 64 * q;
         if (j < g.D) {
           float x = v[u][q];
-          if (ii[q] < g.DT) x = __fadd_rn(__fmul_rn(x, expf(sv[u][q])), tv[u][q]);
+          if (g.strict) {  // x_b + b_1 (x e^s + t), b_1 = 1 - mask
+            const float b1 = ii[q] < g.DT ? 1.f : 0.f;
+            const float w = __fmul_rn(b1, __fadd_rn(__fmul_rn(x, expf(sv[u][q])), tv[u][q]));
+            x = __fadd_rn(__fmul_rn(1.f - b1, x), w);
+            if (j < g.DT) zr[j] = 0.f * x;  // the next layer's x_b (mask 0 here)
+          } else if (ii[q] < g.DT) {
+            x = __fadd_rn(__fmul_rn(x, expf(sv[u][q])), tv[u][q]);
+          }
           zr[g.col(j)] = x;
         }
-        sacc += so[u][q];
+        sacc += g.strict && j >= g.DT ? 0.f * so[u][q] : so[u][q];
       }
-      for (int c = g.DC + lane; c < g.Cp; c += 64) zr[c] = c == g.DC ? 1.f : 0.f;
+      for (int c = g.ones() + lane; c < g.Cp; c += 64) zr[c] = c == g.ones() ? 1.f : 0.f;
       for (int c = g.Cp + g.DT + lane; c < g.Dp; c += 64) zr[c] = 0.f;
       sacc = wave_sum(sacc);
       if (lane == 0) ld[r] = first ? sacc : ldo[u] + sacc;
@@ -634,6 +658,9 @@ __global__ __launch_bounds__(256) void k_wseed(const float* __restrict__ Z,
 //   G_s = g_pre_T x_T e + gld,  G_t = g_pre_T,  g_in_T = g_pre_T e,
 //   g_in_C = g_pre_C (the conditioners' share is added by the first Linear's
 //   back-prop), plus the caller's gradient of the previous layer's output.
+// strict: torch autograd's rules for the op sequence of k_wfwd_update over
+// every feature (b_1 = 1 - mask):  g_v = g b_1, G_t = g_v,
+//   G_s = (g_v x) e + gld b_1,  g_in = g mask + g_v e  (0 * inf = NaN kept).
 // kRU rows per wave with every load of the group issued first (as k_wfwd_update).
 template <int kNJ>
 __global__ __launch_bounds__(256) void k_wbwd_update(
@@ -644,7 +671,7 @@ __global__ __launch_bounds__(256) void k_wbwd_update(
   __shared__ int32_t sq[CNF_MAX_DIM];
   const int32_t* fq = stage_table(sq, fqg, g.D);
   const int lane = threadIdx.x & 63;
-  const int D = g.D, DT = g.DT, DTp = g.DTp;
+  const int D = g.D, DT = g.DT, Op = g.Op;
   int ii[kNJ];
 #pragma unroll
   for (int q = 0; q < kNJ; ++q) ii[q] = lane + 64 * q < D ? fq[lane + 64 * q] : 0;
@@ -661,9 +688,9 @@ __global__ __launch_bounds__(256) void k_wbwd_update(
         vo[u][q] = xt[u][q] = sv[u][q] = gp[u][q] = 0.f;
         if (j < D) {
           vo[u][q] = gout[r * D + j];
-          if (i < DT) {
-            xt[u][q] = X[r * g.Dp + g.Cp + i];
-            if (Os) sv[u][q] = Os[r * DTp + i];
+          if (i < DT || g.strict) {
+            xt[u][q] = X[r * g.Dp + g.col(i)];
+            if (Os) sv[u][q] = Os[r * Op + i];
           }
           if (gprev) gp[u][q] = gprev[r * D + i];
         }
@@ -679,18 +706,25 @@ __global__ __launch_bounds__(256) void k_wbwd_update(
         if (j >= D) continue;
         const float v = vo[u][q];
         float gi = v;
-        if (i < DT) {
+        if (g.strict) {
+          const float b1 = i < DT ? 1.f : 0.f;
           const float e = Os ? expf(sv[u][q]) : 1.f;
-          if (Gs) Gs[r * DTp + i] = __fadd_rn(__fmul_rn(__fmul_rn(v, xt[u][q]), e), gl[u]);
-          if (Gt) Gt[r * DTp + i] = v;
+          const float gv = __fmul_rn(v, b1);
+          if (Gs) Gs[r * Op + i] = __fadd_rn(__fmul_rn(__fmul_rn(gv, xt[u][q]), e), __fmul_rn(gl[u], b1));
+          if (Gt) Gt[r * Op + i] = gv;
+          gi = __fadd_rn(__fmul_rn(v, 1.f - b1), __fmul_rn(gv, e));
+        } else if (i < DT) {
+          const float e = Os ? expf(sv[u][q]) : 1.f;
+          if (Gs) Gs[r * Op + i] = __fadd_rn(__fmul_rn(__fmul_rn(v, xt[u][q]), e), gl[u]);
+          if (Gt) Gt[r * Op + i] = v;
           gi = __fmul_rn(v, e);
         }
         if (gprev) gi += gp[u][q];
         gin[r * D + i] = gi;
       }
-      for (int i = DT + lane; i < DTp; i += 64) {
-        if (Gs) Gs[r * DTp + i] = 0.f;
-        if (Gt) Gt[r * DTp + i] = 0.f;
+      for (int i = (g.strict ? D : DT) + lane; i < Op; i += 64) {
+        if (Gs) Gs[r * Op + i] = 0.f;
+        if (Gt) Gt[r * Op + i] = 0.f;
       }
     }
   }
@@ -806,8 +840,11 @@ F pick_nj(int D, F f1, F f2, F f3, F f4) {
   return D <= 64 ? f1 : (D <= 128 ? f2 : (D <= 192 ? f3 : f4));
 }
 
-int lin_out(const Shape& s, int k) { return k == s.n_lin - 1 ? s.DT : s.units[k + 1]; }
-int lin_in(const Shape& s, int k) { return k == 0 ? s.DC : s.units[k]; }
+// strict: the first Linear sees all D inputs, the last writes all D outputs
+int lin_out(const Shape& s, int k) {
+  return k == s.n_lin - 1 ? (s.strict ? s.D : s.DT) : s.units[k + 1];
+}
+int lin_in(const Shape& s, int k) { return k == 0 ? (s.strict ? s.D : s.DC) : s.units[k]; }
 int hp(const Shape& s, int k) { return r8(s.units[k + 1] + 1); }  // H_k: units + ones
 int gp(const Shape& s, int k) { return r8(lin_out(s, k)); }       // G_k
 
@@ -816,9 +853,11 @@ Geo geo(const Shape& s) {
   g.D = s.D;
   g.DT = s.DT;
   g.DC = s.DC;
-  g.Cp = r8(s.DC + 1);
+  g.strict = s.strict ? 1 : 0;
+  g.Cp = r8((s.strict ? s.D : s.DC) + 1);
   g.DTp = r8(s.DT);
   g.Dp = g.Cp + g.DTp;
+  g.Op = r8(s.strict ? s.D : s.DT);
   return g;
 }
 
@@ -855,7 +894,7 @@ Plan make_plan(const Shape& s, int64_t B) {
   int64_t acts = 0;  // floats of one layer's H / O, all nets
   for (int n = 0; n < s.nets; ++n) {
     for (int k = 0; k + 1 < s.n_lin; ++k) acts += al64(Bn * hp(s, k));
-    acts += al64(Bn * g.DTp);
+    acts += al64(Bn * g.Op);
   }
   p.keep_acts = s.L > 1 && (double)acts * s.L * 4 <= kKeepActsBytes;
   p.act_stride = p.keep_acts ? acts : 0;
@@ -867,7 +906,7 @@ Plan make_plan(const Shape& s, int64_t B) {
       a += al64(Bn * hp(s, k));
     }
     p.O[n] = a;
-    a += al64(Bn * g.DTp);
+    a += al64(Bn * g.Op);
   }
   for (int n = 0; n < s.nets; ++n)
     for (int k = 0; k < s.n_lin; ++k) p.G[n][k] = take(Bn * gp(s, k));
@@ -941,7 +980,7 @@ void gemm(GemmArgs ga, int64_t B, int cols, int K, int nz, bool bt, int epi, boo
 // launch) must fit one CU's LDS: widths up to ~290 (CNF_MAX_WIDTH 512 shapes
 // beyond that keep the torch fallback).
 bool wvjp_ok(const Shape& s) {
-  if (s.strict) return false;
+  if (s.strict && (s.alt_mask || s.s_tanh)) return false;
   constexpr size_t kLds = 160 * 1024;
   for (int k = 0; k < s.n_lin; ++k) {
     const int cols = k == s.n_lin - 1 ? s.DT : hp(s, k);
@@ -1012,12 +1051,12 @@ struct Runner {
         j.A = k == 0 ? Xs(slot) : Hb(slot, n, k - 1);
         j.lda = k == 0 ? Dp : hp(s, k - 1);
         j.K = lin_in(s, k);
-        j.Bw = wptr(layer, n, k) + (k == 0 ? DT : 0);
+        j.Bw = wptr(layer, n, k) + (k == 0 && !s.strict ? DT : 0);
         j.ldb = s.units[k];
         j.N = lin_out(s, k);
         j.bias = bptr(layer, n, k);
         j.C = last ? Ob(slot, n) : Hb(slot, n, k);
-        j.ldc = last ? geom.DTp : hp(s, k);
+        j.ldc = last ? geom.Op : hp(s, k);
         j.ldw = last ? j.N : hp(s, k);
         j.ones = !last;
         j.act = act(n);
@@ -1056,19 +1095,21 @@ struct Runner {
     j.A = Gk(0, 0);
     j.lda = gp(s, 0);
     j.K = lin_out(s, 0);
-    j.Bw = wptr(layer, 0, 0) + DT;
+    const int c0 = s.strict ? 0 : DT;  // strict: every input column (x_b = mask * x)
+    j.Bw = wptr(layer, 0, 0) + c0;
     j.ldb = D;
     if (s.nets == 2) {
       j.A2 = Gk(1, 0);
       j.lda2 = j.lda;
-      j.Bw2 = wptr(layer, 1, 0) + DT;
+      j.Bw2 = wptr(layer, 1, 0) + c0;
       j.ldb2 = D;
     }
-    j.N = DC;
-    j.C = gin + DT;
+    j.N = s.strict ? D : DC;
+    j.C = gin + c0;
+    j.zlt = s.strict ? DT : 0;
     j.ldc = D;
-    j.ldw = DC;
-    gemm(ga, B, DC, j.K, 1, false, kEpiAdd, s.nets == 2, st);
+    j.ldw = j.N;
+    gemm(ga, B, j.N, j.K, 1, false, kEpiAdd, s.nets == 2, st);
   }
 
   // weight / bias gradients of every Linear of both nets (one launch) into the
@@ -1105,7 +1146,8 @@ struct Runner {
         j.cstep = rin ? -1 : 1;
         j.rrev = rout;
         j.nfull = s.units[k + 1];
-        j.woff = n * s.net_floats + lin_off(s, k) + (k == 0 ? (rin ? D - 1 - DT : DT) : 0);
+        j.woff = n * s.net_floats + lin_off(s, k) +
+                 (k == 0 && !s.strict ? (rin ? D - 1 - DT : DT) : 0);
         j.wld = s.units[k];
         j.boff = n * s.net_floats + lin_off(s, k) + (int64_t)s.units[k + 1] * s.units[k];
         j.tiles_c = (j.K + 1 + 31) / 32;
@@ -1194,7 +1236,7 @@ int wvjp_run(const Shape& s, const void* prepared, const float* x, const int64_t
 int wvjp_inv_run(const Shape& s, const void* prepared, const float* z, const float* gx,
                  const float* gx_all, const float* gld_in, float* grads, float* dz, int64_t B,
                  void* ws, size_t ws_bytes, hipStream_t st) {
-  if (!wvjp_ok(s)) return CNF_ERR_UNSUPPORTED;
+  if (!wvjp_ok(s) || s.strict) return CNF_ERR_UNSUPPORTED;  // strict: forward reverse mode only
   const Plan p = make_plan(s, B);
   if (!ws || ws_bytes < (size_t)p.total * 4) return CNF_ERR_NULL;
   if (B == 0) return empty_batch(s, grads, nullptr, st);

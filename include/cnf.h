@@ -138,8 +138,10 @@ int cnf_forward_loss(const cnf_desc* desc, const void* prepared, const float* x,
  *   log_priors [D]     DEVICE pointer (the calibrator's log class priors)
  *   probs      [B][D]  calibrated probabilities
  *   logdet     [B]     log-det of the centred rows, may be NULL
- * Narrow flows (the k_sgpr shapes) without random_flip; CNF_ERR_UNSUPPORTED
- * otherwise (the caller composes cnf_forward with its own softmax). */
+ * Served by k_sgpr (the narrow shapes, random_flip included) and k_wide (the
+ * wide shapes of its table, e.g. D=100, hidden [100,100]); CNF_ERR_UNSUPPORTED
+ * otherwise (strict_nan, legacy options, other wide shapes: the caller then
+ * composes cnf_forward with its own softmax). */
 int cnf_predict(const cnf_desc* desc, const void* prepared, const float* x,
                 const float* log_priors, float* probs, float* logdet, int64_t B, void* stream);
 

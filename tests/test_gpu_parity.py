@@ -387,7 +387,10 @@ def test_fused_predict_matches_reference_formula(D, hidden, L, flip):
     """cnf_predict (one launch: centring, flow, softmax, prior correction) vs the
     reference's Calibrator.predict math (calibrators.py:40-44, 350-352) in fp64
     on the flow's fp32 outputs."""
-    f = _make_flow(D, L, hidden, 0.1, 4, random_flip=flip)
+    # 100-wide Linears at N(0, 0.1) make the flow chaotic: the last-ulp
+    # difference between the kernel's in-launch centring and torch's mean
+    # grows past 1e-5 in the probabilities; the wide case runs at N(0, 0.03)
+    f = _make_flow(D, L, hidden, 0.1 if D <= 16 else 0.03, 4, random_flip=flip)
     stack = f._native_stack()
     g = torch.Generator(device=DEV).manual_seed(8)
     x = torch.randn(5000, D, device=DEV, generator=g) * 3 + 1
@@ -396,7 +399,7 @@ def test_fused_predict_matches_reference_formula(D, hidden, L, flip):
     n0 = engine.stats["predict"]
     probs = stack.predict(x, lp)
     fused = engine.stats["predict"] == n0 + 1
-    assert fused == (D <= 16 and not flip)   # other shapes compose cnf_forward + torch ops
+    assert fused  # one cnf_predict launch: k_sgpr (random_flip too) or k_wide (D=100)
     with torch.no_grad():
         z, _ = f.transform(x - x.mean(dim=1, keepdim=True))
     p = torch.softmax(z.double(), dim=1).cpu()

@@ -1,0 +1,124 @@
+"""Native reverse mode of strict_nan stacks (cnf_desc.strict_nan, the
+reference's inf * 0 = NaN at masked positions, flows/flows.py:101-112): the
+layer-at-a-time kernels of cnf_wvjp.hip follow torch autograd's rules for the
+reference's op sequence over every feature.  Gradients must match CPU autograd
+of the reference's own ops, NaN / inf positions included, through the
+cnf::flow operator (C++ autograd), through ctypes (cnf_vjp) and through the
+fused loss (cnf_loss_vjp)."""
+import numpy as np
+import pytest
+import torch
+
+from _golden import load
+from _model import build_flow
+from cnf_hip import _lib, engine
+from cnf_hip import vjp as V
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _same(got, ref, name):
+    got, ref = got.detach().cpu().double(), ref.detach().cpu().double()
+    assert got.shape == ref.shape, name
+    assert torch.equal(torch.isnan(got), torch.isnan(ref)), (name, torch.isnan(got).sum().item(),
+                                                             torch.isnan(ref).sum().item())
+    assert torch.equal(torch.isinf(got), torch.isinf(ref)), name
+    fin = torch.isfinite(ref)
+    if fin.any():
+        scale = ref[fin].abs().max().item() + 1e-30
+        assert (got[fin] - ref[fin]).abs().max().item() <= 1e-4 * scale + 1e-7, name
+
+
+def _case(kind):
+    """(flow state, x, y): the g6_d4_nan fixture (masked exp(s) = inf in every
+    row) or a variant where only some rows overflow."""
+    meta, state, d = load("g6_d4_nan")
+    x = torch.from_numpy(d["x"])
+    y = torch.from_numpy(d["y"])
+    if kind == "some_rows":
+        # s at the masked feature = 200 (w . h) + 88: exp(s) overflows in the rows
+        # where w . h > 0.0036 (37 of the 64 at x * 8), the others stay finite
+        state = dict(state)
+        b = np.array(state["layers.0.s.layers.1.bias"], copy=True)
+        w = np.array(state["layers.0.s.layers.1.weight"], copy=True)
+        b[-1] = 88.0
+        w[-1] *= 200.0
+        state["layers.0.s.layers.1.bias"] = b
+        state["layers.0.s.layers.1.weight"] = w
+        x = x * 8.0
+    return meta, state, x, y
+
+
+def _cpu_grads(meta, state, x, y, objective):
+    f = build_flow(meta, state, "cpu", strict_nan=True)
+    xx = x.clone().requires_grad_(True)
+    out = objective(f, xx, y)
+    ps = [p for p in f.parameters() if p.requires_grad]
+    gs = torch.autograd.grad(out, ps + [xx], allow_unused=True)
+    return out.detach(), [torch.zeros_like(p) if g is None else g for g, p in zip(gs, ps + [xx])]
+
+
+def _loss(f, x, y):
+    z, ld = f.transform(x)
+    p = torch.softmax(z, 1).gather(1, y.view(-1, 1)).squeeze(1)
+    return -torch.mean(torch.log(p + 1e-7) + ld)
+
+
+def _zs_objective(f, x, y):
+    # gradient through every layer output (the zs list) and the log-det
+    zs, ld = f(x)
+    w = torch.arange(1, x.shape[1] + 1, dtype=x.dtype, device=x.device)
+    return sum(((z * w).sum() for z in zs), torch.zeros((), device=x.device)) + 0.5 * ld.sum()
+
+
+@pytest.mark.parametrize("kind", ["fixture", "some_rows"])
+@pytest.mark.parametrize("objective", ["loss", "zs"])
+@pytest.mark.parametrize("via_ops", [True, False])
+def test_strict_vjp_matches_cpu_autograd(kind, objective, via_ops, monkeypatch):
+    monkeypatch.setattr(engine, "USE_TORCH_OPS", via_ops)
+    meta, state, x, y = _case(kind)
+    obj = _loss if objective == "loss" else _zs_objective
+    ref_out, ref = _cpu_grads(meta, state, x, y, obj)
+    f = build_flow(meta, state, DEV, strict_nan=True)
+    assert f._native_stack().has_native_vjp(), "strict stacks must have a native reverse mode"
+    xx = x.to(DEV).requires_grad_(True)
+    n0 = engine.stats["vjp"]
+    out = obj(f, xx, y.to(DEV))
+    ps = [p for p in f.parameters() if p.requires_grad]
+    got = torch.autograd.grad(out, ps + [xx], allow_unused=True)
+    torch.cuda.synchronize()
+    if not via_ops:
+        assert engine.stats["vjp"] > n0, "native cnf_vjp did not run"
+    if kind == "some_rows":  # the case must really mix NaN and finite rows
+        assert torch.isnan(ref[-1]).any(1).any() and not torch.isnan(ref[-1]).any(1).all()
+    _same(out, ref_out, "objective")
+    for i, (g, r) in enumerate(zip(got, ref)):
+        _same(torch.zeros_like(r) if g is None else g, r, "grad %d" % i)
+
+
+@pytest.mark.parametrize("kind", ["fixture", "some_rows"])
+def test_strict_fused_loss_vjp_matches_cpu_autograd(kind):
+    meta, state, x, y = _case(kind)
+    ref_out, ref = _cpu_grads(meta, state, x, y, _loss)
+    f = build_flow(meta, state, DEV, strict_nan=True)
+    stack = f._native_stack()
+    B = x.shape[0]
+    terms, grads, dx = V.loss_and_grads(stack, x.to(DEV), y.to(DEV), grad_scale=1.0 / B,
+                                        need_dx=True)
+    flat = torch.cat([g.reshape(-1) for g in ref[:-1]])
+    _same(grads, flat, "grads")
+    _same(dx, ref[-1], "dx")
+    _same(terms[0] / B, ref_out, "loss")
+
+
+def test_strict_inverse_vjp_stays_unsupported():
+    """Autograd through the strict INVERSE keeps the torch fallback (the ABI
+    reports it unsupported rather than computing non-strict gradients)."""
+    meta, state, _, _ = _case("fixture")
+    f = build_flow(meta, state, DEV, strict_nan=True)
+    import ctypes
+    n = ctypes.c_size_t()
+    st = _lib.lib().cnf_vjp_inverse_workspace_bytes(ctypes.byref(f._native_stack().desc),
+                                                    ctypes.c_int64(4), ctypes.byref(n))
+    assert st == -3
