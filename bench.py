@@ -352,29 +352,60 @@ def measured_traffic(workload, B, mode):
     return best
 
 
-def cpu_baseline(w, seconds=10.0):
-    """The op-for-op torch CPU port (oracle/cnf_torch_port.py) on host cores."""
+def _cpu_share():
+    """CPUs this process may use: the affinity mask, capped by a cgroup v2
+    CPU quota when one is set (the GPU box grants a share of a larger host)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) / int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_baseline(w, seconds=10.0, rounds=7):
+    """The op-for-op torch CPU port (oracle/cnf_torch_port.py) on host cores:
+    `rounds` interleaved rounds over two thread counts -- torch's default
+    (OMP_NUM_THREADS, 16 on the GPU box) and every CPU this process may use --
+    one timed pass of the config's full batch per count and round; the
+    reported value is the faster count's median, both medians are listed."""
     from oracle import cnf_torch_port as P
     flow = make_flow(w, "cpu")
     st = {k: v for k, v in flow.state_dict().items()}
     layers = P.layers_from_state(st, w["L"], len(w["hidden"]) + 1, w["scale"], True)
     B = w["B"]  # the config's own batch (2^20 for cfg2)
     x, _ = synthetic_logits(B, w["D"], "cpu", 99)
-    P.flow_forward(layers, x)
-    times = []
-    t_start = time.perf_counter()
-    while time.perf_counter() - t_start < seconds or len(times) < 3:
-        t = time.perf_counter()
+    default = torch.get_num_threads()
+    counts = sorted({default, _cpu_share()})
+    times = {c: [] for c in counts}
+    for c in counts:  # warm each pool once
+        torch.set_num_threads(c)
         P.flow_forward(layers, x)
-        times.append(time.perf_counter() - t)
-    rate = B / float(np.median(times))
-    return {"value": rate, "unit": "logit-vectors/sec", "cores": torch.get_num_threads(),
-            "nproc": os.cpu_count(), "kind": "port",
-            "sample": "%d x %d-vector forward passes (the config's B, D=%d, L=%d, h=%s) with the "
-                      "op-for-op torch CPU port on %d torch threads of a %d-CPU host, median; "
+    t_start = time.perf_counter()
+    r = 0
+    while r < rounds or (time.perf_counter() - t_start < seconds and r < 4 * rounds):
+        for c in counts:
+            torch.set_num_threads(c)
+            t = time.perf_counter()
+            P.flow_forward(layers, x)
+            times[c].append(time.perf_counter() - t)
+        r += 1
+    torch.set_num_threads(default)
+    med = {c: float(np.median(v)) for c, v in times.items()}
+    best = min(med, key=med.get)
+    return {"value": B / med[best], "unit": "logit-vectors/sec", "cores": best,
+            "nproc": os.cpu_count(), "cpu_share": _cpu_share(),
+            "by_threads": {str(c): round(B / med[c], 1) for c in counts},
+            "kind": "port",
+            "sample": "%d interleaved rounds x %d-vector forward passes (the config's B, D=%d, "
+                      "L=%d, h=%s) with the op-for-op torch CPU port at %s torch threads (this "
+                      "process's CPU share: %d of a %d-CPU host), median per thread count; "
                       "port/reference time ratio: profiles/*_cpu_port_ratio.jsonl, DESIGN.md"
-                      % (len(times), B, w["D"], w["L"], w["hidden"], torch.get_num_threads(),
-                         os.cpu_count() or 0)}
+                      % (r, B, w["D"], w["L"], w["hidden"], " and ".join(map(str, counts)),
+                         _cpu_share(), os.cpu_count() or 0)}
 
 
 def free_port():

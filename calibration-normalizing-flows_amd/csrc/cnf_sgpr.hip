@@ -38,9 +38,11 @@
 //     (global_load_lds_dwordx4, no VGPRs) while the current tile computes; a
 //     lane's two rows are 2*D contiguous floats, so each feature pair is one
 //     ds_read2_b32 straight into a packed register pair;
-//   * output: the lane's 2*D contiguous output floats leave as 16-B stores from
-//     registers, issued one tile LATE (after the next tile's LDS reads), so the
-//     wave's wait for its DMA never waits on stores it has just issued;
+//   * output: the lane writes its rows into the wave's LDS tile (the input
+//     tile's rows are in registers by then, ds_write2_b32 per feature pair),
+//     and the wave stores the tile lane-linear with streaming 16-B stores, each
+//     instruction 1 KiB contiguous; the next tile's LDS-DMA is issued once the
+//     staged rows have been read back (kStage 1 below);
 //   * a persistent grid (CUs x resident blocks) walks the tiles wave by wave;
 //     s_setprio by tiles remaining (longest-remaining-first) keeps the SIMDs'
 //     oldest-first arbitration from leaving a long single-wave tail.

@@ -476,6 +476,93 @@ __global__ __launch_bounds__(64, 2) void k_vjp2(const float* __restrict__ W,
     f2 gld = zero;
     auto seed = [&](auto O_) __attribute__((always_inline)) {
       constexpr bool O = decltype(O_)::value;
+#ifndef CNF_V2_SCALAR_SEED
+      if constexpr (LOSS) {
+        // Both rows as packed pairs (k_sgpr's pair_loss form): the max, the
+        // exponentials e_j = exp(z_j - m) (kept: p_j = e_j / se, no second
+        // exp pass), the sum, and the gradient scale(coef) * p_j.  The rows'
+        // z[y] come from the wave's LDS tile (the lane's two rows at tile
+        // [0, D) and [D, 2D), as the input was read), and the one-hot
+        // subtraction g_y -= scale * coef is an LDS add at that slot before
+        // the pairs are read back -- no per-row select trees.
+        typedef __attribute__((address_space(3))) float lds_f;
+        const uint32_t tb = (uint32_t)(uintptr_t)(lds_f*)(tile + 2 * D * lane);
+        wave_sync();  // every lane's rows were read from the tile long ago
+#pragma unroll
+        for (int j = 0; j < D; ++j)
+          asm volatile("ds_write2_b32 %0, %1, %2 offset0:%3 offset1:%4" ::"v"(tb),
+                       "v"(v[R<D, O>(j)].x), "v"(v[R<D, O>(j)].y), "i"(j), "i"(D + j)
+                       : "memory");
+        const uint32_t b0 = lab & 0xffu, b1 = (lab >> 8) & 0xffu;
+        const bool ok[2] = {b0 != 0xffu, b1 != 0xffu};
+        const int yy[2] = {ok[0] ? (int)b0 : 0, ok[1] ? (int)b1 : 0};
+        float zy[2];
+        zy[0] = tile[2 * D * lane + yy[0]];
+        zy[1] = tile[2 * D * lane + D + yy[1]];
+        f2 m = v[R<D, O>(0)];
+#pragma unroll
+        for (int j = 1; j < D; ++j) m = maxT(m, v[R<D, O>(j)]);
+        const f2 nm = m * splat(-kL2E, f2{});
+        f2 e[D], se = zero;
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+          e[j] = exp2T(fmaT(kL2E, v[R<D, O>(j)], nm));
+          se += e[j];
+        }
+        f2 sc;  // grad_scale * coef / se per row
+        float dy[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const float lse = m[q] + __builtin_amdgcn_logf(se[q]) * kLN2;
+          const float lpy = zy[q] - lse;
+          const bool valid = q < nr;
+          const float ldq = NETS == 2 ? ld[q] : 0.f;
+          float coef, ce_term, loss_row, gl;
+          if (a.kind == CNF_LOSS_CAL) {  // -(log(softmax(z)[y] + 1e-7) + ld)
+            const float py = __builtin_amdgcn_exp2f(lpy * kL2E);
+            ce_term = -__builtin_amdgcn_logf(py + kEps) * kLN2;
+            loss_row = ce_term - ldq;
+            coef = py / (py + kEps);
+            gl = -a.grad_scale;
+          } else {                       // CE(z, y) - det * ld
+            ce_term = -lpy;
+            loss_row = ce_term - a.det * ldq;
+            coef = 1.f;
+            gl = -a.det * a.grad_scale;
+          }
+          if (!ok[q]) ce_term = loss_row = coef = __builtin_nanf("");
+          if (!valid) coef = gl = 0.f;
+          sc[q] = a.grad_scale * coef / se[q];
+          dy[q] = -a.grad_scale * coef;
+          gld[q] = gl;
+          if (valid) {
+            lt0 += loss_row;
+            lt1 += ce_term;
+            lt2 += ldq;
+          }
+        }
+        // g_j = sc e_j, then g_y += dy: staged over the z rows (same slots)
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+          const f2 gj = e[j] * sc;
+          asm volatile("ds_write2_b32 %0, %1, %2 offset0:%3 offset1:%4" ::"v"(tb), "v"(gj.x),
+                       "v"(gj.y), "i"(j), "i"(D + j)
+                       : "memory");
+        }
+        asm volatile("ds_add_f32 %0, %1" ::"v"(tb + 4u * yy[0]), "v"(dy[0]) : "memory");
+        asm volatile("ds_add_f32 %0, %1 offset:%2" ::"v"(tb + 4u * yy[1]), "v"(dy[1]), "i"(4 * D)
+                     : "memory");
+#pragma unroll
+        for (int j = 0; j < D; ++j)
+          asm volatile("ds_read2_b32 %0, %1 offset0:%2 offset1:%3"
+                       : "=v"(g[R<D, O>(j)])
+                       : "v"(tb), "i"(j), "i"(D + j)
+                       : "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int j = 0; j < D; ++j) asm volatile("" : "+v"(g[R<D, O>(j)]));
+      } else
+#endif
       if constexpr (LOSS) {
 #pragma unroll
         for (int q = 0; q < 2; ++q) {

@@ -439,6 +439,135 @@ __global__ __launch_bounds__(256, 3) void k_wdw(DwArgs da) {
   }
 }
 
+// The same weight gradients on v_mfma_f32_16x16x4f32 tiles (the same 64
+// FLOP/clk/SIMD as 32x32x2): a wave still owns 32 output rows, and up to 112
+// columns, as 16 x 16 tiles, so a job's padding is to the next 16 instead of 32 --
+// N = 100 needs 7 row tiles (112) instead of 4 x 32 (128), the 101 columns
+// of [H | 1] 7 column tiles (112) instead of 128: the (100, 101) job issues
+// 49 tiles' MFMAs instead of 64, a cfg4 layer 18 % fewer in all.  Operand
+// loads per 16 rows are unchanged (K-step s: lane (i, q) reads G[row 4s + q]
+// [n + i] and H[row 4s + q][c + i], 64 contiguous bytes per quarter-wave).
+constexpr int kDw16CT = 7;  // 16-column tiles per wave (112 columns: [H | 1] of a 100-wide layer)
+
+__global__ __launch_bounds__(256, 3) void k_wdw16(DwArgs da) {
+  const DwJob j = da.job[blockIdx.y];
+  const int lane = threadIdx.x & 63, i = lane & 15, kq = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tiles16 = (j.K + 1 + 15) >> 4;
+  const int nsub = (j.N + 31) >> 5, ncg = (tiles16 + kDw16CT - 1) / kDw16CT;
+  const int gn = (int)blockIdx.z / ncg, cg = (int)blockIdx.z % ncg;
+  const int ns = gn * 4 + w;
+  if (gn * 4 >= nsub || ns >= nsub) return;  // no __syncthreads below: waves may leave
+  const int n0 = ns * 32, c0 = cg * 16 * kDw16CT;
+  const int nrs = n0 + 16 < j.N ? 2 : 1;  // 16-row tiles of this wave (wave-uniform)
+  const int nct = min(kDw16CT, tiles16 - cg * kDw16CT);
+  const int64_t r0 = (int64_t)blockIdx.x * da.rows;
+  const int64_t r1 = min(da.M, r0 + da.rows);
+  if (r0 >= r1) return;
+  const int ldg = (int)j.ldg, ldh = (int)j.ldh;
+  int goff[2], hoff[kDw16CT];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) goff[t] = (kq * ldg + min(n0 + 16 * t + i, j.N - 1)) * 4;
+#pragma unroll
+  for (int c = 0; c < kDw16CT; ++c) hoff[c] = (kq * ldh + min(c0 + 16 * c + i, ldh - 1)) * 4;
+  // 16-row chunks (4 MFMA k-steps of 4 rows) in two operand sets used in turn
+  constexpr int KS = 4;
+  auto load = [&](int64_t mr, float (&a)[2][KS], float (&b)[kDw16CT][KS]) {
+    const auto gr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(j.G + mr * ldg), 0,
+                                                      0x7fffffff, 0x00020000);
+    const auto hr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(j.H + mr * ldh), 0,
+                                                      0x7fffffff, 0x00020000);
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+      if (t < nrs) {
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+          a[t][s] = __builtin_bit_cast(
+              float, __builtin_amdgcn_raw_buffer_load_b32(gr, goff[t], 4 * s * ldg * 4, 0));
+      }
+#pragma unroll
+    for (int c = 0; c < kDw16CT; ++c)
+      if (c < nct) {
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+          b[c][s] = __builtin_bit_cast(
+              float, __builtin_amdgcn_raw_buffer_load_b32(hr, hoff[c], 4 * s * ldh * 4, 0));
+      }
+  };
+  auto mfmas = [&](f4 (&acc)[2][kDw16CT], const float (*a)[KS], const float (*b)[KS]) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+      if (t < nrs) {
+#pragma unroll
+        for (int c = 0; c < kDw16CT; ++c)
+          if (c < nct) {
+#pragma unroll
+            for (int s = 0; s < KS; ++s)
+              acc[t][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][s], b[c][s], acc[t][c], 0, 0, 0);
+          }
+      }
+  };
+  f4 acc[2][kDw16CT];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int c = 0; c < kDw16CT; ++c) acc[t][c] = f4{};
+  const int64_t rfull = r0 + (r1 - r0) / 16 * 16;  // rows in whole chunks
+  if (rfull > r0) {
+    float a0[2][KS], b0[kDw16CT][KS], a1[2][KS], b1[kDw16CT][KS];
+    load(r0, a0, b0);
+    for (int64_t mr = r0;; mr += 32) {
+      const bool more1 = mr + 16 < rfull;
+      if (more1) load(mr + 16, a1, b1);
+      __builtin_amdgcn_sched_barrier(0);
+      mfmas(acc, a0, b0);
+      if (!more1) break;
+      const bool more2 = mr + 32 < rfull;
+      if (more2) load(mr + 32, a0, b0);
+      __builtin_amdgcn_sched_barrier(0);
+      mfmas(acc, a1, b1);
+      if (!more2) break;
+    }
+  }
+  if (rfull < r1) {  // the batch's ragged end: rows past r1 contribute zero
+    float a[2][KS], b[kDw16CT][KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int64_t row = rfull + 4 * s + kq;
+      const bool ok = row < r1;
+      const int64_t rr = ok ? row : r1 - 1;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) a[t][s] = ok ? j.G[rr * ldg + min(n0 + 16 * t + i, j.N - 1)] : 0.f;
+#pragma unroll
+      for (int c = 0; c < kDw16CT; ++c) b[c][s] = j.H[rr * ldh + min(c0 + 16 * c + i, ldh - 1)];
+    }
+    mfmas(acc, a, b);
+  }
+  // lane (i, kq), register q of tile (t, c): dW row n0 + 16 t + 4 kq + q, column c0 + 16 c + i
+  float* out = da.partials + (int64_t)blockIdx.x * da.PS;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    if (t >= nrs) continue;
+#pragma unroll
+    for (int c = 0; c < kDw16CT; ++c) {
+      const int k = c0 + c * 16 + i;
+      if (c >= nct || k > j.K) continue;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int nn = n0 + 16 * t + 4 * kq + q;
+        if (nn >= j.N) continue;
+        const int pr = j.rrev ? j.nfull - 1 - nn : nn;  // parameter row
+        if (k < j.K) out[j.woff + (int64_t)pr * j.wld + (int64_t)j.cstep * k] = acc[t][c][q];
+        else out[j.boff + pr] = acc[t][c][q];
+      }
+    }
+  }
+}
+
+#ifndef CNF_WDW16
+#define CNF_WDW16 1  // A/B: 0 keeps the 32x32 tiles of k_wdw
+#endif
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -1151,11 +1280,14 @@ struct Runner {
         j.wld = s.units[k];
         j.boff = n * s.net_floats + lin_off(s, k) + (int64_t)s.units[k + 1] * s.units[k];
         j.tiles_c = (j.K + 1 + 31) / 32;
-        max_subs = std::max(max_subs, ((j.N + 127) / 128) * ((j.tiles_c + kDwCT - 1) / kDwCT));
+        const int ncg = CNF_WDW16 ? ((j.K + 1 + 15) / 16 + kDw16CT - 1) / kDw16CT
+                                  : (j.tiles_c + kDwCT - 1) / kDwCT;
+        max_subs = std::max(max_subs, ((j.N + 127) / 128) * ncg);
       }
     }
-    hipLaunchKernelGGL(k_wdw, dim3((unsigned)p.nkb, (unsigned)jobs, (unsigned)max_subs),
-                       dim3(256), 0, st, da);
+    hipLaunchKernelGGL(CNF_WDW16 ? k_wdw16 : k_wdw,
+                       dim3((unsigned)p.nkb, (unsigned)jobs, (unsigned)max_subs), dim3(256), 0, st,
+                       da);
     reduce_partials(part, (int)p.nkb, (int)PS, (int)PL, grads_layer, nullptr, st);
     return CNF_OK;
   }

@@ -78,8 +78,10 @@ typedef struct cnf_desc {
  *             parameters keep the layer's own column / row order;
  *   S_TANH    the s-net's hidden activations are tanh (code-old/realNVP.py:
  *             58-64); the t-net keeps ReLU.
- * Served by the MFMA-tile family (forward / inverse) and its reverse mode;
- * not combinable with random_flip permutations. */
+ * Forward / inverse: k_valu for the narrow shapes of its tables (the code-old
+ * default hidden=[dim] at D=3 and 10, and [5,5]), the MFMA-tile family for
+ * every other shape; reverse mode: the layer-at-a-time kernels of
+ * cnf_wvjp.hip.  Not combinable with random_flip permutations or strict_nan. */
 #define CNF_OPT_ALT_MASK 4
 #define CNF_OPT_S_TANH 8
 
