@@ -102,6 +102,11 @@ bool wide_ok(const Shape& s);               // k_wide serves this descriptor's f
 int wide_prepare(const Shape& s, const float* const* params, void* prepared, hipStream_t st);
 int wide_run(const Shape& s, const void* prepared, const float* in, float* out, float* ld,
              int64_t B, bool inverse, hipStream_t st, const float* log_priors = nullptr);
+// the 16x16x4-tile implementation behind wide_* (cnf_wide16.hip)
+int64_t wide16_layer_floats(const Shape& s);
+int wide16_prepare(const Shape& s, const float* const* params, void* prepared, hipStream_t st);
+int wide16_run(const Shape& s, const void* prepared, const float* in, float* out, float* ld,
+               int64_t B, bool inverse, hipStream_t st, const float* log_priors);
 
 // layer-at-a-time MFMA reverse mode of the tile family (cnf_wvjp.hip)
 bool wvjp_ok(const Shape& s);

@@ -490,7 +490,15 @@ size_t wide_lds(const Shape& s) { return (size_t)kWWaves * (kWRows * (s.D | 1) +
 
 }  // namespace
 
+// CNF_WIDE16 (default): the wide_* entry points run k_wide16 (16x16x4 tiles,
+// cnf_wide16.hip) for every shape of the table; 0 keeps k_wide's 32x32x2
+// tiles (A/B builds).
+#ifndef CNF_WIDE16
+#define CNF_WIDE16 1
+#endif
+
 int64_t wide_layer_floats(const Shape& s) {
+  if (CNF_WIDE16) return wfind(s) ? wide16_layer_floats(s) : 0;
   const WEntry* e = wfind(s);
   return e ? (int64_t)e->net_floats * s.nets : 0;
 }
@@ -503,6 +511,7 @@ bool wide_ok(const Shape& s) {
 }
 
 int wide_prepare(const Shape& s, const float* const* params, void* prepared, hipStream_t st) {
+  if (CNF_WIDE16) return wfind(s) ? wide16_prepare(s, params, prepared, st) : CNF_OK;
   const WEntry* e = wfind(s);
   if (!e) return CNF_OK;
   float* region = reinterpret_cast<float*>(static_cast<char*>(prepared) + idx_bytes(s)) +
@@ -538,6 +547,8 @@ int wide_prepare(const Shape& s, const float* const* params, void* prepared, hip
 
 int wide_run(const Shape& s, const void* prepared, const float* in, float* out, float* ld,
              int64_t B, bool inverse, hipStream_t st, const float* log_priors) {
+  if (CNF_WIDE16) return wfind(s) ? wide16_run(s, prepared, in, out, ld, B, inverse, st, log_priors)
+                                  : CNF_ERR_UNSUPPORTED;
   const WEntry* e = wfind(s);
   if (!e) return CNF_ERR_UNSUPPORTED;
   const char* base = static_cast<const char*>(prepared);
