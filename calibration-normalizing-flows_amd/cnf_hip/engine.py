@@ -116,8 +116,9 @@ class CouplingStack:
         return "valu-fused" if all_outputs and name == "sgpr-fused" else name
 
     def has_native_vjp(self):
-        """True when cnf_vjp serves this descriptor (strict_nan stacks, for
-        one, have no native reverse mode).  Cached: support depends only on the
+        """True when cnf_vjp serves this descriptor (every shape within the
+        ABI's limits, strict_nan included, except strict stacks under the legacy
+        alternate mask or tanh s-net).  Cached: support depends only on the
         shape and options."""
         if self._vjp_ok is None:
             n = ctypes.c_size_t()

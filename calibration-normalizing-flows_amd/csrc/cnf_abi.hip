@@ -296,7 +296,7 @@ int cnf_vjp_inverse_workspace_bytes(const cnf_desc* desc, int64_t B, size_t* byt
   if (!bytes) return CNF_ERR_NULL;
   if (B < 0) return CNF_ERR_BATCH;
   if (s.strict) return CNF_ERR_UNSUPPORTED;  // strict: the forward's reverse mode only
-  return wvjp_workspace(s, B, bytes);
+  return wvjp_inv_workspace(s, B, bytes);
 }
 
 int cnf_vjp_inverse(const cnf_desc* desc, const void* prepared, const float* z, const float* gx,

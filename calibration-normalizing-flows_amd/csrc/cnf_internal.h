@@ -102,6 +102,35 @@ bool wide_ok(const Shape& s);               // k_wide serves this descriptor's f
 int wide_prepare(const Shape& s, const float* const* params, void* prepared, hipStream_t st);
 int wide_run(const Shape& s, const void* prepared, const float* in, float* out, float* ld,
              int64_t B, bool inverse, hipStream_t st, const float* log_priors = nullptr);
+// Training of the wide stacks (cnf_wide16.hip): per-row tape / gradient
+// layouts in floats (parts at -1 are absent).  Nets in natural order: 0 the
+// s-net, 1 the t-net (one net: the t-net).  Every part is in slot order: unit
+// u of a 16-unit tile sits at slot 16 (u >> 4) + 4 (u & 3) + ((u & 15) >> 2).
+struct WTrain16Layout {
+  int RW, GW;         // tape / gradient floats per row
+  int xc, cw;         // conditioning half [x_C | 1], width
+  int xt, s, ts;      // transformed half before the update, s-net output, width
+  int h[2][3], hw[3]; // net n's hidden k (1..NL-1) [relu(h_k) | 1], width
+  int glast[2];       // gradient of net n's output (width ts)
+  int gpre[2][3], gpw[3];  // gradient of hidden k's pre-activation, width
+};
+// The tape and G arrays are wave-tiled: rows in blocks of 32 (allocated whole),
+// a block's 32 x W floats as [W / 16 tiles][2][16 rows][16 slots] (row r =
+// 32 w + 16 g + i, column c at w * 32 W + (c >> 4) * 512 + g * 256 + i * 16 +
+// (c & 15)); one array of a layer is wide16_blocks(B) * 32 * W floats.
+int wide16_train_layout(const Shape& s, WTrain16Layout* out);
+inline int64_t wide16_blocks(int64_t B) { return (B + 31) / 32; }
+// tbits: relu' bits, 512 words per 32 rows and layer (wide16_tbits_words)
+int wide16_train_forward(const Shape& s, const void* prepared, const float* x, float* zst, int Cp,
+                         int Dp, float* ld, float* tape, uint32_t* tbits, int64_t B,
+                         hipStream_t st);
+// the reverse sweep of every layer (one launch); gz: the seed (gradient of
+// the last output), gz_all: [L][B][D] or null, dx: or null; gbuf: L x B x GW
+int wide16_train_backward(const Shape& s, const void* prepared, const float* gz,
+                          const float* gz_all, float* dx, const float* gld, const float* tape,
+                          const uint32_t* tbits, float* gbuf, int64_t B, hipStream_t st);
+inline int64_t wide16_tbits_words(int64_t B) { return (B + 31) / 32 * 512; }  // per layer
+bool wide16_train_ok(const Shape& s);  // the fused training sweeps serve this descriptor
 // the 16x16x4-tile implementation behind wide_* (cnf_wide16.hip)
 int64_t wide16_layer_floats(const Shape& s);
 int wide16_prepare(const Shape& s, const float* const* params, void* prepared, hipStream_t st);
@@ -111,6 +140,7 @@ int wide16_run(const Shape& s, const void* prepared, const float* in, float* out
 // layer-at-a-time MFMA reverse mode of the tile family (cnf_wvjp.hip)
 bool wvjp_ok(const Shape& s);
 int wvjp_workspace(const Shape& s, int64_t B, size_t* bytes);
+int wvjp_inv_workspace(const Shape& s, int64_t B, size_t* bytes);
 int wvjp_run(const Shape& s, const void* prepared, const float* x, const int64_t* y,
              const float* gz, const float* gz_all, const float* gld, int kind, float det,
              float grad_scale, float* loss_terms, float* grads, float* dx, int64_t B, void* ws,

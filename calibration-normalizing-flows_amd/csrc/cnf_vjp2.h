@@ -426,7 +426,6 @@ __global__ __launch_bounds__(64, 2) void k_vjp2(const float* __restrict__ W,
     f2 ld = zero;
     auto fwd = [&](auto O_, int l) __attribute__((always_inline)) {
       constexpr bool O = decltype(O_)::value;
-      const float* wl = W + (int64_t)l * LF;
       f2 c[DC];
 #pragma unroll
       for (int k = 0; k < DC; ++k) c[k] = v[R<D, O>(DT + k)];

@@ -510,6 +510,8 @@ bool wide_ok(const Shape& s) {
          !(s.options & CNF_OPT_NO_WIDE);
 }
 
+bool wide16_train_ok(const Shape& s) { return CNF_WIDE16 && wide_ok(s); }
+
 int wide_prepare(const Shape& s, const float* const* params, void* prepared, hipStream_t st) {
   if (CNF_WIDE16) return wfind(s) ? wide16_prepare(s, params, prepared, st) : CNF_OK;
   const WEntry* e = wfind(s);

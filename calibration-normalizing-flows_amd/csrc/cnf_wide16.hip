@@ -61,6 +61,7 @@ __host__ __device__ constexpr int cdiv(int a, int b) { return (a + b - 1) / b; }
 // Compile-time geometry of one conditioner MLP (H = 0: absent hidden layer).
 template <int D, int H1, int H2>
 struct G16 {
+  static constexpr bool kBias = true;  // Linears with biases (the forward)
   static constexpr int DT = D / 2, DC = D - D / 2;
   static constexpr int NL = H1 == 0 ? 1 : (H2 == 0 ? 2 : 3);
   static constexpr int CT = cdiv(DC, 16), CS = 16 * CT;  // conditioning tiles / slots
@@ -107,7 +108,8 @@ __device__ __forceinline__ void wsync() {
 // K-step N of M-tile MO of Linear I of net NET: A from the prefetch ring,
 // refilled P fragments ahead along the layer's A stream (both nets, every
 // Linear) and on into the next layer's (an).  Both row groups.
-template <class G, int NETS, int NET, int I, int MO, int N, int P, int TIN>
+// The B operand is tile TOFF + N / 4 of `in`.
+template <class G, int NETS, int NET, int I, int MO, int N, int TOFF, int P, int TIN>
 __device__ __forceinline__ void kstep(v4 (&acc)[2], float (&ring)[P], const float* __restrict__ a,
                                       const float* __restrict__ an, const v4 (&in)[TIN][2]) {
   constexpr int LS = NETS * G::steps();
@@ -115,7 +117,7 @@ __device__ __forceinline__ void kstep(v4 (&acc)[2], float (&ring)[P], const floa
   const float av = ring[T % P];
   if constexpr (T + P < LS) ring[T % P] = a[(T + P) * 64];
   else ring[T % P] = an[(T + P - LS) * 64];
-  constexpr int t = N >> 2, q = N & 3;
+  constexpr int t = TOFF + (N >> 2), q = N & 3;
   acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, in[t][0][q], acc[0], 0, 0, 0);
   acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, in[t][1][q], acc[1], 0, 0, 0);
   // keep each refill where it is (left alone, the scheduler sinks the loads
@@ -125,9 +127,13 @@ __device__ __forceinline__ void kstep(v4 (&acc)[2], float (&ring)[P], const floa
 
 // Epilogues of an M-tile's accumulators: hidden (ReLU), keep (the t-net's
 // output), or the fused affine update of the state (the s-net's last Linear).
+// pre<MO>() runs before M-tile MO's K-steps (operand prefetch), put<MO>(acc)
+// after them.
 template <bool RELU, int TOUT>
 struct EpOut {
   v4 (&o)[TOUT][2];
+  template <int MO>
+  __device__ __forceinline__ void pre() {}
   template <int MO>
   __device__ __forceinline__ void put(v4 (&acc)[2]) {
 #pragma unroll
@@ -147,6 +153,8 @@ struct EpAffine {
   const v4 (&T)[TT][2];
   float (&ld)[2];
   template <int MO>
+  __device__ __forceinline__ void pre() {}
+  template <int MO>
   __device__ __forceinline__ void put(v4 (&s)[2]) {
 #pragma unroll
     for (int g = 0; g < 2; ++g)
@@ -162,33 +170,42 @@ struct EpAffine {
   }
 };
 
-// accumulators of M-tile MO of Linear I start at its biases (the layer's bias
-// block: 16 floats per M-tile in slot order)
+// M-tile MO of Linear I's biases (the layer's bias block: 16 floats per M-tile
+// in slot order), loaded when the tile starts and added after its K-steps, so
+// the load's latency hides under them (a bias-initialised accumulator made
+// every M-tile's first MFMA wait for memory)
 template <class G, int I, int MO>
-__device__ __forceinline__ void bias_init(v4 (&acc)[2], const float* __restrict__ bias, int lane) {
-  const float* p = bias + G::bbefore(I) + 16 * MO + 4 * (lane >> 4);
-  const v4 b = {p[0], p[1], p[2], p[3]};
-  acc[0] = b;
-  acc[1] = b;
+__device__ __forceinline__ v4 bias_load(const float* __restrict__ bias, int lane) {
+  if constexpr (!G::kBias) {
+    return v4{0.f, 0.f, 0.f, 0.f};
+  } else {
+    const float* p = bias + G::bbefore(I) + 16 * MO + 4 * (lane >> 4);
+    return v4{p[0], p[1], p[2], p[3]};
+  }
 }
 
-template <class G, int NETS, int NET, int I, int MO, int P, int TIN, class EP, int... N>
+template <class G, int NETS, int NET, int I, int MO, int TOFF, int P, int TIN, class EP, int... N>
 __device__ __forceinline__ void mtile(float (&ring)[P], const float* __restrict__ a,
                                       const float* __restrict__ an,
                                       const float* __restrict__ bias, const v4 (&in)[TIN][2],
                                       EP& ep, int lane, std::integer_sequence<int, N...>) {
-  v4 acc[2];
-  bias_init<G, I, MO>(acc, bias, lane);
-  (kstep<G, NETS, NET, I, MO, N, P>(acc, ring, a, an, in), ...);
+  v4 acc[2] = {v4{0.f, 0.f, 0.f, 0.f}, v4{0.f, 0.f, 0.f, 0.f}};
+  ep.template pre<MO>();
+  const v4 b = bias_load<G, I, MO>(bias, lane);
+  (kstep<G, NETS, NET, I, MO, N, TOFF, P>(acc, ring, a, an, in), ...);
+  if constexpr (G::kBias) {
+    acc[0] += b;
+    acc[1] += b;
+  }
   ep.template put<MO>(acc);
 }
 
-template <class G, int NETS, int NET, int I, int P, int TIN, class EP, int... M>
+template <class G, int NETS, int NET, int I, int TOFF, int P, int TIN, class EP, int... M>
 __device__ __forceinline__ void lin(float (&ring)[P], const float* __restrict__ a,
                                     const float* __restrict__ an, const float* __restrict__ bias,
                                     const v4 (&in)[TIN][2], EP& ep, int lane,
                                     std::integer_sequence<int, M...>) {
-  (mtile<G, NETS, NET, I, M>(ring, a, an, bias, in, ep, lane,
+  (mtile<G, NETS, NET, I, M, TOFF>(ring, a, an, bias, in, ep, lane,
                              std::make_integer_sequence<int, G::ks(I)>{}),
    ...);
 }
@@ -201,21 +218,21 @@ __device__ __forceinline__ void net(float (&ring)[P], const float* __restrict__ 
                                     const v4 (&X)[G::XT][2], EP& ep, int lane) {
   using MS0 = std::make_integer_sequence<int, G::mt(0)>;
   if constexpr (G::NL == 1) {
-    lin<G, NETS, NET, 0>(ring, a, an, bias, X, ep, lane, MS0{});
+    lin<G, NETS, NET, 0, 0>(ring, a, an, bias, X, ep, lane, MS0{});
   } else if constexpr (G::NL == 2) {
     v4 h1[G::T1][2];
     EpOut<true, G::T1> e1{h1};
-    lin<G, NETS, NET, 0>(ring, a, an, bias, X, e1, lane, MS0{});
-    lin<G, NETS, NET, 1>(ring, a, an, bias, h1, ep, lane,
+    lin<G, NETS, NET, 0, 0>(ring, a, an, bias, X, e1, lane, MS0{});
+    lin<G, NETS, NET, 1, 0>(ring, a, an, bias, h1, ep, lane,
                          std::make_integer_sequence<int, G::mt(1)>{});
   } else {
     v4 h1[G::T1][2], h2[G::T2][2];
     EpOut<true, G::T1> e1{h1};
     EpOut<true, G::T2> e2{h2};
-    lin<G, NETS, NET, 0>(ring, a, an, bias, X, e1, lane, MS0{});
-    lin<G, NETS, NET, 1>(ring, a, an, bias, h1, e2, lane,
+    lin<G, NETS, NET, 0, 0>(ring, a, an, bias, X, e1, lane, MS0{});
+    lin<G, NETS, NET, 1, 0>(ring, a, an, bias, h1, e2, lane,
                          std::make_integer_sequence<int, G::mt(1)>{});
-    lin<G, NETS, NET, 2>(ring, a, an, bias, h2, ep, lane,
+    lin<G, NETS, NET, 2, 0>(ring, a, an, bias, h2, ep, lane,
                          std::make_integer_sequence<int, G::mt(2)>{});
   }
 }
@@ -320,7 +337,8 @@ __global__ __launch_bounds__(64 * kWaves, 2) void k_wide16(
   constexpr int S = D | 1;  // odd LDS row stride
   constexpr int LA = NETS * G::NA, LF = LA + NETS * G::NB;  // A floats / all floats per layer
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // SGPR: row0, descriptors
   const int64_t row0 = ((int64_t)blockIdx.x * kWaves + wave) * kRows;
   if (row0 >= B) return;  // waves synchronise only with themselves
   const int nrows = (int)((B - row0) < kRows ? (B - row0) : kRows);
@@ -403,39 +421,594 @@ __global__ __launch_bounds__(64 * kWaves, 2) void k_wide16(
 }
 
 // ---------------------------------------------------------------------------
+// Training (cnf_vjp / cnf_loss_vjp of these shapes): the forward sweep as
+// above plus a per-row tape, then one reverse-sweep launch per layer whose
+// transposed products run on the same register tiles.  Replaces autograd of
+// flows/flows.py:101-112 and flows/utils.py:26-31 for the stacks in the table.
+// ---------------------------------------------------------------------------
+
+// Reverse-mode chain of one conditioner, last Linear first: step i is the
+// transposed product of forward Linear f = NL-1-i (input: the gradient of f's
+// output, nout_f units; output: the gradient of f's input, nin_f units).  No
+// biases: accumulators start at 0.
+template <int D, int H1, int H2>
+struct G16T {
+  using F = G16<D, H1, H2>;
+  static constexpr bool kBias = false;
+  static constexpr int DT = F::DT, DC = F::DC, NL = F::NL, CT = F::CT, TT = F::TT, XT = F::XT;
+  static constexpr int nin(int i) { return F::nout(NL - 1 - i); }
+  static constexpr int nout(int i) { return F::nin(NL - 1 - i); }
+  static constexpr int ks(int i) { return cdiv(nin(i), 4); }
+  static constexpr int mt(int i) { return cdiv(nout(i), 16); }
+  static constexpr int sbefore(int i) { return i == 0 ? 0 : sbefore(i - 1) + mt(i - 1) * ks(i - 1); }
+  static constexpr int steps() { return sbefore(NL); }
+  static constexpr int bbefore(int) { return 0; }
+  static constexpr int NA = steps() * 64;
+};
+
+// Per-row tape of one layer, every part in slot order (16-slot tiles), so the
+// reverse sweep reads back exactly the register tiles the forward held:
+//   XC  conditioning half, 1 at unit DC (the bias column of dW)  16 cdiv(DC+1, 16)
+//   XT  transformed half before the update                       16 TT
+//   S   the s-net's output (NETS == 2)                           16 TT
+//   H   per net n, hidden k = 1..NL-1: relu(h_k), 1 at unit H_k  16 cdiv(H_k+1, 16)
+// and the reverse sweep's per-row conditioner gradients (the dW operands):
+//   per net n: G_last (of its output, 16 TT), then per hidden k the gradient of
+//   h_k's pre-activation (16 cdiv(H_k, 16)).
+// Nets in natural order: 0 the s-net, 1 the t-net (NETS == 1: the t-net).
+template <int D, int H1, int H2, int NETS>
+struct Tape16 {
+  using F = G16<D, H1, H2>;
+  static constexpr int CW = 16 * cdiv(F::DC + 1, 16);
+  static constexpr int TS = 16 * F::TT;
+  static constexpr int HW(int k) { return 16 * cdiv(F::hid(k) + 1, 16); }
+  static constexpr int XC = 0, XTo = CW, So = CW + TS;
+  static constexpr int H0 = So + (NETS == 2 ? TS : 0);
+  static constexpr int netH = (F::NL > 1 ? HW(1) : 0) + (F::NL > 2 ? HW(2) : 0);
+  static constexpr int H(int n, int k) { return H0 + n * netH + (k == 2 ? HW(1) : 0); }
+  static constexpr int RW = 16 * cdiv(H0 + NETS * netH, 16);
+  static constexpr int GP(int k) { return 16 * cdiv(F::hid(k), 16); }
+  static constexpr int netG = TS + (F::NL > 1 ? GP(1) : 0) + (F::NL > 2 ? GP(2) : 0);
+  static constexpr int Glast(int n) { return n * netG; }
+  static constexpr int Gpre(int n, int k) { return n * netG + TS + (k == 2 ? GP(1) : 0); }
+  static constexpr int GW = NETS * netG;
+};
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+// A/B knobs (never shipped changed): which tape traffic runs -- bit 0 the
+// XC / XT / S stores, 1 the hidden stores, 2 the reverse sweep's G stores --
+// and the stores' cache-policy bits
+#ifndef CNF_W16_TAPE
+#define CNF_W16_TAPE 15
+#endif
+#ifndef CNF_W16_STORE_AUX
+#define CNF_W16_STORE_AUX 0
+#endif
+
+// One wave's block of a wave-tiled [B][W] array (the tape and G layouts):
+// rows in blocks of 32, a block's 32 x W floats as [W / 16 tiles][2 row
+// groups][16 rows][16 slots], so row r = 32 w + 16 g + i, column c sits at
+//   w * 32 W + (c >> 4) * 512 + g * 256 + i * 16 + (c & 15)
+// and one tile store of a row group is one contiguous KiB (row-major [B][W]
+// rows took 64-B pieces of 16 rows per store: 0.68 ms more per cfg4 forward
+// sweep).  Lane (i, k) of row group g addresses row 16 g + i, slots 4k..4k+3.
+// Arrays are allocated in whole blocks: a ragged wave's rows past the batch
+// read and write the padding.
+struct Rows16 {
+  __amdgpu_buffer_rsrc_t rs;
+  int voff[2];
+  __device__ __forceinline__ Rows16(const float* block, int W, int lane) {
+    rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(block), 0, kRows * W * 4, 0x00020000);
+#pragma unroll
+    for (int g = 0; g < 2; ++g) voff[g] = (g * 256 + (lane & 15) * 16 + 4 * (lane >> 4)) * 4;
+  }
+  // off: the tile's first slot (floats into the row, a multiple of 16)
+  __device__ __forceinline__ void store(const v4& v, int g, int off) const {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), rs, voff[g], off * 128,
+                                           CNF_W16_STORE_AUX);
+  }
+  __device__ __forceinline__ v4 load(int g, int off) const {
+    return __builtin_bit_cast(v4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff[g], off * 128, 0));
+  }
+};
+
+// slot ONE of a tile set to 1 in lane group (ONE >> 2) & 3 (the ones column)
+template <int ONE, int MO>
+__device__ __forceinline__ v4 with_one(v4 v, int lane) {
+  if constexpr ((ONE >> 4) == MO) {
+    if ((lane >> 4) == ((ONE >> 2) & 3)) v[ONE & 3] = 1.f;
+  }
+  return v;
+}
+
+// Tape traffic and the vector-memory counter.  A wave waits for its A-ring
+// loads with vmcnt, which counts loads and stores alike and in issue order:
+// every store or tape load must complete within the P K-steps that separate
+// a ring load from its use, or it stalls the MFMA stream (measured: per-tile
+// stores and relu' loads cost the reverse sweep 156 us per cfg4 layer, the
+// forward's hidden stores 97 us).  So the sweeps issue tape stores in bursts,
+// one per Linear (the tiles are live anyway: the next Linear's input), and
+// the reverse sweep takes relu' from BITS written by the forward -- one bit
+// per activation, every hidden layer of a layer in 8 words per lane, loaded
+// once when the launch starts -- instead of loading the activations per tile.
+
+// relu' bits of hidden layer word pair WI (4 words per net and lane): bit
+// 8 (MO & 3) + 4 g + q of word WI + (MO >> 2) is (h > 0) for register q, row
+// group g of M-tile MO (hidden widths up to 128)
+template <int WI, int MO>
+__device__ __forceinline__ void put_bits(uint32_t (&mb)[4], const v4 (&h)[2]) {
+  static_assert(MO < 8, "relu' bits cover 8 tiles");
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (h[g][q] > 0.f) mb[WI + (MO >> 2)] |= 1u << (8 * (MO & 3) + 4 * g + q);
+}
+template <int WI, int MO>
+__device__ __forceinline__ bool get_bit(const uint32_t (&mb)[8], int g, int q) {
+  return (mb[WI + (MO >> 2)] >> (8 * (MO & 3) + 4 * g + q)) & 1u;
+}
+
+// hidden Linear of the forward sweep: ReLU, keep the tile, record relu'
+template <int TOUT, int WI>
+struct EpTape {
+  v4 (&o)[TOUT][2];
+  uint32_t (&mb)[4];
+  template <int MO>
+  __device__ __forceinline__ void pre() {}
+  template <int MO>
+  __device__ __forceinline__ void put(v4 (&acc)[2]) {
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[g][q] = fmaxf(acc[g][q], 0.f);
+      o[MO][g] = acc[g];
+    }
+    put_bits<WI, MO>(mb, acc);
+  }
+};
+
+// one burst of T tiles into part OFF (slot ONE of the part set to 1)
+template <int OFF, int T, int ONE>
+__device__ __forceinline__ void tape_tiles(const Rows16& tp, const v4 (&h)[T][2], int lane) {
+  if (!(CNF_W16_TAPE & 2)) return;
+#pragma unroll
+  for (int t = 0; t < T; ++t)
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      v4 v = h[t][g];
+      if ((ONE >> 4) == t && (lane >> 4) == ((ONE >> 2) & 3)) v[ONE & 3] = 1.f;
+      tp.store(v, g, OFF + 16 * t);
+    }
+}
+
+// a part's extra tile holding only the ones column (width a multiple of 16)
+template <int OFF, int T, int ONE>
+__device__ __forceinline__ void tape_ones_tile(const Rows16& tp, int lane) {
+  if constexpr ((ONE >> 4) == T) {
+#pragma unroll
+    for (int g = 0; g < 2; ++g) tp.store(with_one<ONE, T>(v4{0.f, 0.f, 0.f, 0.f}, lane), g, OFF + 16 * T);
+  }
+}
+
+// the s-net's last Linear: tape s, then the affine update (as EpAffine)
+template <int XT, int CT, int TT, int OFF>
+struct EpAffineTape {
+  v4 (&X)[XT][2];
+  const v4 (&T)[TT][2];
+  float (&ld)[2];
+  const Rows16& tp;
+  template <int MO>
+  __device__ __forceinline__ void pre() {}
+  template <int MO>
+  __device__ __forceinline__ void put(v4 (&s)[2]) {
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      if (CNF_W16_TAPE & 1) tp.store(s[g], g, OFF + 16 * MO);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float sv = s[g][q];
+        const float e = __builtin_amdgcn_exp2f(sv * 1.4426950408889634f);
+        X[CT + MO][g][q] = fmaf(X[CT + MO][g][q], e, T[MO][g][q]);
+        ld[g] += sv;
+      }
+    }
+  }
+};
+
+// One conditioner of the forward sweep (stream position POS, tape net N)
+// (relu' bits of hidden k: words 2 (k - 1), +1 of the net's four, stored to
+// bits[4 N ..] of the wave's lane record when the net is done)
+template <class G, class TP, int NETS, int POS, int N, int P, class EP>
+__device__ __forceinline__ void net_tape(float (&ring)[P], const float* __restrict__ a,
+                                         const float* __restrict__ an,
+                                         const float* __restrict__ bias,
+                                         const v4 (&X)[G::XT][2], EP& ep, const Rows16& tp,
+                                         uint32_t* __restrict__ bits, int lane) {
+  using MS0 = std::make_integer_sequence<int, G::mt(0)>;
+  if constexpr (G::NL == 1) {
+    lin<G, NETS, POS, 0, 0>(ring, a, an, bias, X, ep, lane, MS0{});
+  } else {
+    uint32_t mb[4] = {0u, 0u, 0u, 0u};
+    constexpr int O1 = qslot(G::hid(1));
+    v4 h1[G::T1][2];
+    EpTape<G::T1, 0> e1{h1, mb};
+    lin<G, NETS, POS, 0, 0>(ring, a, an, bias, X, e1, lane, MS0{});
+    tape_tiles<TP::H(N, 1), G::T1, O1>(tp, h1, lane);
+    tape_ones_tile<TP::H(N, 1), G::T1, O1>(tp, lane);
+    if constexpr (G::NL == 2) {
+      lin<G, NETS, POS, 1, 0>(ring, a, an, bias, h1, ep, lane,
+                              std::make_integer_sequence<int, G::mt(1)>{});
+    } else {
+      constexpr int O2 = qslot(G::hid(2));
+      v4 h2[G::T2][2];
+      EpTape<G::T2, 2> e2{h2, mb};
+      lin<G, NETS, POS, 1, 0>(ring, a, an, bias, h1, e2, lane,
+                              std::make_integer_sequence<int, G::mt(1)>{});
+      tape_tiles<TP::H(N, 2), G::T2, O2>(tp, h2, lane);
+      tape_ones_tile<TP::H(N, 2), G::T2, O2>(tp, lane);
+      lin<G, NETS, POS, 2, 0>(ring, a, an, bias, h2, ep, lane,
+                              std::make_integer_sequence<int, G::mt(2)>{});
+    }
+    *reinterpret_cast<v4i*>(bits + 4 * N) = v4i{(int)mb[0], (int)mb[1], (int)mb[2], (int)mb[3]};
+  }
+}
+
+// Forward sweep of training: k_wide16's forward with the tape of every layer
+// written on the way (stores interleaved with the MFMAs), the final output in
+// the stash layout the loss seed reads (column Cp + f for f < DT, f - DT
+// otherwise; row stride Dp) and each row's log-det.
+template <int D, int H1, int H2, int NETS>
+__global__ __launch_bounds__(64 * kWaves, 2) void k_wtrain16_fwd(
+    const float* __restrict__ W, const int32_t* __restrict__ qtab, const float* __restrict__ in,
+    float* __restrict__ zst, float* __restrict__ ld_out, float* __restrict__ tape,
+    uint32_t* __restrict__ tbits, int64_t B, int L, int Cp, int Dp) {
+  using G = G16<D, H1, H2>;
+  using TP = Tape16<D, H1, H2, NETS>;
+  constexpr int XT = G::XT, CT = G::CT, TT = G::TT;
+  constexpr int S = D | 1;
+  constexpr int LA = NETS * G::NA, LF = LA + NETS * G::NB;
+  constexpr int OC = qslot(G::DC);
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // SGPR: row0, descriptors
+  const int64_t row0 = ((int64_t)blockIdx.x * kWaves + wave) * kRows;
+  if (row0 >= B) return;
+  const int nrows = (int)((B - row0) < kRows ? (B - row0) : kRows);
+  const int64_t nwb = (B + kRows - 1) / kRows;
+  float* st = smem + wave * (kRows * S + D);
+  int* qs = reinterpret_cast<int*>(st + kRows * S);
+
+  const float* src = in + row0 * D;
+  for (int i = lane; i < kRows * D; i += 64) {
+    const int r = i / D, f = i - r * D;
+    st[r * S + f] = r < nrows ? src[i] : 0.f;
+  }
+  wsync();
+  v4 X[XT][2];
+  get_state<G>(st, S, nullptr, X, lane);
+  wsync();
+
+  constexpr int P = ring16(NETS * G::steps(), CNF_W16_PMAX);
+  float ring[P];
+#pragma unroll
+  for (int j = 0; j < P; ++j) ring[j] = W[lane + j * 64];
+  float ld[2] = {0.f, 0.f};
+  for (int l = 0; l < L; ++l) {
+    const int ln = l + 1 < L ? l + 1 : l;
+    const float* __restrict__ wl = W + (int64_t)l * LF + lane;
+    const float* __restrict__ wn = W + (int64_t)ln * LF + lane;
+    const float* __restrict__ bl = W + (int64_t)l * LF + LA;
+    const Rows16 tp(tape + ((int64_t)l * nwb * kRows + row0) * TP::RW, TP::RW, lane);
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+#pragma unroll
+      for (int t = 0; t < CT; ++t) {
+        v4 v = X[t][g];
+        if ((OC >> 4) == t && (lane >> 4) == ((OC >> 2) & 3)) v[OC & 3] = 1.f;
+        if (CNF_W16_TAPE & 1) tp.store(v, g, TP::XC + 16 * t);
+      }
+#pragma unroll
+      for (int t = 0; t < TT; ++t)
+        if (CNF_W16_TAPE & 1) tp.store(X[CT + t][g], g, TP::XTo + 16 * t);
+    }
+    tape_ones_tile<TP::XC, CT, OC>(tp, lane);
+    v4 Tv[TT][2];
+    EpOut<false, TT> et{Tv};
+    // this wave's relu' bits: 8 words per lane (4 per net)
+    uint32_t* bp = tbits + ((int64_t)l * nwb + row0 / kRows) * 512 + lane * 8;
+    if constexpr (NETS == 2) {  // forward stream: t-net (tape net 1), then s-net (net 0)
+      net_tape<G, TP, 2, 0, 1>(ring, wl, wn, bl, X, et, tp, bp, lane);
+      EpAffineTape<XT, CT, TT, TP::So> ea{X, Tv, ld, tp};
+      net_tape<G, TP, 2, 1, 0>(ring, wl, wn, bl + G::NB, X, ea, tp, bp, lane);
+    } else {
+      net_tape<G, TP, 1, 0, 0>(ring, wl, wn, bl, X, et, tp, bp, lane);
+#pragma unroll
+      for (int t = 0; t < TT; ++t)
+#pragma unroll
+        for (int g = 0; g < 2; ++g) X[CT + t][g] = X[CT + t][g] + Tv[t][g];
+    }
+    relayout<G>(st, qs, S, qtab + l * D, X, lane);
+  }
+
+  put_state<G>(st, S, X, lane);
+  wsync();
+  for (int i = lane; i < nrows * D; i += 64) {
+    const int r = i / D, f = i - r * D;
+    zst[(row0 + r) * Dp + (f < G::DT ? Cp + f : f - G::DT)] = st[r * S + f];
+  }
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    ld[g] += __shfl_xor(ld[g], 16);
+    ld[g] += __shfl_xor(ld[g], 32);
+  }
+  if (lane < 16) {
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+      if (16 * g + lane < nrows) ld_out[row0 + 16 * g + lane] = ld[g];
+  }
+}
+
+// reverse sweep, hidden step: relu'(h) from the forward's bits (torch's
+// threshold backward: h <= 0 -> 0), keep the tile (stored as a dW operand in
+// one burst after the Linear)
+template <int TOUT, int WI>
+struct EpMaskTape {
+  v4 (&o)[TOUT][2];
+  const uint32_t (&mb)[8];
+  template <int MO>
+  __device__ __forceinline__ void pre() {}
+  template <int MO>
+  __device__ __forceinline__ void put(v4 (&acc)[2]) {
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[g][q] = get_bit<WI, MO>(mb, g, q) ? acc[g][q] : 0.f;
+      o[MO][g] = acc[g];
+    }
+  }
+};
+
+template <int OFF, int T>
+__device__ __forceinline__ void g_tiles(const Rows16& gb, const v4 (&h)[T][2]) {
+  if (!(CNF_W16_TAPE & 4)) return;
+#pragma unroll
+  for (int t = 0; t < T; ++t)
+#pragma unroll
+    for (int g = 0; g < 2; ++g) gb.store(h[t][g], g, OFF + 16 * t);
+}
+
+// reverse sweep, first Linear: the conditioners' share of the gradient of the
+// conditioning half, added to the state's tiles
+template <int XT>
+struct EpAddC {
+  v4 (&X)[XT][2];
+  template <int MO>
+  __device__ __forceinline__ void pre() {}
+  template <int MO>
+  __device__ __forceinline__ void put(v4 (&acc)[2]) {
+#pragma unroll
+    for (int g = 0; g < 2; ++g) X[MO][g] = X[MO][g] + acc[g];
+  }
+};
+
+// Back through one conditioner (net N, reverse-stream position N) from the
+// gradient of its output (tiles TOFF.. of `in`) into the state's C tiles.
+template <class GT, class TP, int NETS, int N, int TOFF, int P, int TIN, int XT>
+__device__ __forceinline__ void net_back(float (&ring)[P], const float* __restrict__ a,
+                                         const float* __restrict__ an,
+                                         const v4 (&in)[TIN][2], v4 (&X)[XT][2],
+                                         const uint32_t (&mb)[8], const Rows16& gb, int lane) {
+  EpAddC<XT> ec{X};
+  using MS0 = std::make_integer_sequence<int, GT::mt(0)>;
+  if constexpr (GT::NL == 1) {
+    lin<GT, NETS, N, 0, TOFF>(ring, a, an, nullptr, in, ec, lane, MS0{});
+  } else if constexpr (GT::NL == 2) {
+    v4 g1[GT::mt(0)][2];
+    EpMaskTape<GT::mt(0), 4 * N> e0{g1, mb};
+    lin<GT, NETS, N, 0, TOFF>(ring, a, an, nullptr, in, e0, lane, MS0{});
+    g_tiles<TP::Gpre(N, 1), GT::mt(0)>(gb, g1);
+    lin<GT, NETS, N, 1, 0>(ring, a, an, nullptr, g1, ec, lane,
+                           std::make_integer_sequence<int, GT::mt(1)>{});
+  } else {
+    v4 g2[GT::mt(0)][2];
+    EpMaskTape<GT::mt(0), 4 * N + 2> e0{g2, mb};
+    lin<GT, NETS, N, 0, TOFF>(ring, a, an, nullptr, in, e0, lane, MS0{});
+    g_tiles<TP::Gpre(N, 2), GT::mt(0)>(gb, g2);
+    v4 g1[GT::mt(1)][2];
+    EpMaskTape<GT::mt(1), 4 * N> e1{g1, mb};
+    lin<GT, NETS, N, 1, 0>(ring, a, an, nullptr, g2, e1, lane,
+                           std::make_integer_sequence<int, GT::mt(1)>{});
+    g_tiles<TP::Gpre(N, 1), GT::mt(1)>(gb, g1);
+    lin<GT, NETS, N, 2, 0>(ring, a, an, nullptr, g1, ec, lane,
+                           std::make_integer_sequence<int, GT::mt(2)>{});
+  }
+}
+
+// The reverse sweep, every layer in one launch (last first), 32 rows per wave;
+// the gradient state stays in registers from layer to layer and the A ring
+// runs on from one layer's transposed stream into the next.  Per layer l:
+//   g_out (+ the caller's gradient of z_l when l < L-1) is gathered back
+//   through the flip / permutation (iq = fq^-1, one LDS pass);
+//   with e = e^s:  G_s = g_T x_T e + gld,  G_t = g_T,  g_in_T = g_T e,
+//   g_in_C = g_C + the conditioners' share (their transposed chains, relu'
+//   from the forward's bits).
+// Every Linear's output gradient goes to layer l's G rows (the dW operands).
+// gz: the seed (gradient of z_{L-1}, natural order); dx (optional): the
+// gradient of the flow's input.
+template <int D, int H1, int H2, int NETS>
+__global__ __launch_bounds__(64 * kWaves, 2) void k_wtrain16_bwd(
+    const float* __restrict__ WT, const int32_t* __restrict__ iqtab, const float* __restrict__ gz,
+    const float* __restrict__ gz_all, float* __restrict__ dx, const float* __restrict__ gld,
+    const float* __restrict__ tape, const uint32_t* __restrict__ tbits, float* __restrict__ gbuf,
+    int64_t B, int L) {
+  using G = G16<D, H1, H2>;
+  using GT = G16T<D, H1, H2>;
+  using TP = Tape16<D, H1, H2, NETS>;
+  constexpr int XT = G::XT, CT = G::CT, TT = G::TT;
+  constexpr int S = D | 1;
+  constexpr int LT = NETS * GT::NA;  // transposed-stream floats per layer
+  constexpr float kL2E = 1.4426950408889634f;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // SGPR: row0, descriptors
+  const int64_t row0 = ((int64_t)blockIdx.x * kWaves + wave) * kRows;
+  if (row0 >= B) return;
+  const int nrows = (int)((B - row0) < kRows ? (B - row0) : kRows);
+  const int64_t nwb = (B + kRows - 1) / kRows;
+  float* st = smem + wave * (kRows * S + D);
+  int* qs = reinterpret_cast<int*>(st + kRows * S);
+
+  const float* src = gz + row0 * D;
+  for (int i = lane; i < kRows * D; i += 64) {
+    const int r = i / D, f = i - r * D;
+    st[r * S + f] = r < nrows ? src[i] : 0.f;
+  }
+  constexpr int P = ring16(NETS * GT::steps(), CNF_W16_PMAX);
+  float ring[P];
+  {
+    const float* a0 = WT + (int64_t)(L - 1) * LT + lane;
+#pragma unroll
+    for (int j = 0; j < P; ++j) ring[j] = a0[j * 64];
+  }
+  float gl[2];
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    const int r = 16 * g + (lane & 15);
+    gl[g] = r < nrows ? gld[row0 + r] : 0.f;
+  }
+  v4 X[XT][2];
+  for (int l = L - 1; l >= 0; --l) {
+    // this layer's relu' bits (issued first, used late)
+    uint32_t mb[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    if constexpr (G::NL > 1) {
+      const uint32_t* bp = tbits + ((int64_t)l * nwb + row0 / kRows) * 512 + lane * 8;
+      const v4i b0 = *reinterpret_cast<const v4i*>(bp);
+      mb[0] = b0[0], mb[1] = b0[1], mb[2] = b0[2], mb[3] = b0[3];
+      if constexpr (NETS == 2) {
+        const v4i b1 = *reinterpret_cast<const v4i*>(bp + 4);
+        mb[4] = b1[0], mb[5] = b1[1], mb[6] = b1[2], mb[7] = b1[3];
+      }
+    }
+    const Rows16 tp(tape + ((int64_t)l * nwb * kRows + row0) * TP::RW, TP::RW, lane);
+    const Rows16 gb(gbuf + ((int64_t)l * nwb * kRows + row0) * TP::GW, TP::GW, lane);
+    v4 xv[TT][2], sv[TT][2];
+#pragma unroll
+    for (int t = 0; t < TT; ++t)
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        xv[t][g] = tp.load(g, TP::XTo + 16 * t);
+        if constexpr (NETS == 2) sv[t][g] = tp.load(g, TP::So + 16 * t);
+      }
+    // g_out of layer l in LDS (natural order): the caller's gradient of z_l
+    // joins it, then the gather through iq
+    for (int j = lane; j < D; j += 64) qs[j] = iqtab[l * D + j];
+    if (gz_all && l < L - 1) {
+      const float* gp = gz_all + ((int64_t)l * B + row0) * D;
+      for (int i = lane; i < nrows * D; i += 64) {
+        const int r = i / D, f = i - r * D;
+        st[r * S + f] += gp[i];
+      }
+    }
+    wsync();
+    get_state<G>(st, S, qs, X, lane);
+    wsync();
+    const float* __restrict__ wa = WT + (int64_t)l * LT + lane;
+    const float* __restrict__ wn = WT + (int64_t)(l > 0 ? l - 1 : l) * LT + lane;
+    if constexpr (NETS == 2) {
+      v4 Gs[TT][2];
+#pragma unroll
+      for (int t = 0; t < TT; ++t)
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float e = __builtin_amdgcn_exp2f(sv[t][g][q] * kL2E);
+            const bool real = 16 * t + 4 * q + (lane >> 4) < G::DT;
+            Gs[t][g][q] = real ? __fadd_rn(__fmul_rn(__fmul_rn(X[CT + t][g][q], xv[t][g][q]), e), gl[g])
+                               : 0.f;
+          }
+          gb.store(Gs[t][g], g, TP::Glast(0) + 16 * t);
+          gb.store(X[CT + t][g], g, TP::Glast(1) + 16 * t);
+        }
+      net_back<GT, TP, 2, 0, 0>(ring, wa, wn, Gs, X, mb, gb, lane);   // s-net
+      net_back<GT, TP, 2, 1, CT>(ring, wa, wn, X, X, mb, gb, lane);   // t-net: G_t = g_T
+      // g_in_T = g_T e (s reloaded: the tape part is read-only here)
+#pragma unroll
+      for (int t = 0; t < TT; ++t)
+#pragma unroll
+        for (int g = 0; g < 2; ++g) sv[t][g] = tp.load(g, TP::So + 16 * t);
+#pragma unroll
+      for (int t = 0; t < TT; ++t)
+#pragma unroll
+        for (int g = 0; g < 2; ++g)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            X[CT + t][g][q] = __fmul_rn(X[CT + t][g][q], __builtin_amdgcn_exp2f(sv[t][g][q] * kL2E));
+    } else {
+#pragma unroll
+      for (int t = 0; t < TT; ++t)
+#pragma unroll
+        for (int g = 0; g < 2; ++g) gb.store(X[CT + t][g], g, TP::Glast(0) + 16 * t);
+      net_back<GT, TP, 1, 0, CT>(ring, wa, wn, X, X, mb, gb, lane);
+    }
+    put_state<G>(st, S, X, lane);  // g_in: the gradient of z_{l-1} (natural order)
+    wsync();
+  }
+  if (dx) {
+    float* dst = dx + row0 * D;
+    for (int i = lane; i < nrows * D; i += 64) {
+      const int r = i / D, f = i - r * D;
+      dst[i] = st[r * S + f];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
 using WFn = void (*)(const float*, const int32_t*, const float*, float*, float*, int64_t, int,
                     const float*);
+using TFwdFn = void (*)(const float*, const int32_t*, const float*, float*, float*, float*,
+                        uint32_t*, int64_t, int, int, int);
+using TBwdFn = void (*)(const float*, const int32_t*, const float*, const float*, float*,
+                        const float*, const float*, const uint32_t*, float*, int64_t, int);
 
 // One Linear's A / bias recipe for the prepare kernel.
 struct WSeg16 {
   const float* W;
   const float* b;
-  int64_t adst, bdst;     // float offsets of its A fragments and bias block
+  int64_t adst, bdst;     // float offsets of its A fragments and bias block (-1: none)
   int nm, nk;             // M-tiles, K-steps
-  int first;              // input = the conditioning half (weight columns DT..D-1)
-  int nin, nout;          // real input / output units
-  int nin_full;           // the reference weight is [nout][nin_full]
+  int first;              // the Linear reads the conditioning half (weight columns DT..D-1)
+  int trans;              // the transposed product (reverse sweep): out = the Linear's input
+  int nin, nout;          // real input / output units of the product
+  int nin_full;           // the reference weight is [nout][nin_full] (forward sense)
   int DT;
 };
 struct WPrep16 {
-  WSeg16 seg[6];  // 2 nets x up to 3 Linears
+  WSeg16 seg[12];  // 2 nets x up to 3 Linears, forward and transposed
   int nseg;
 };
 
-// A fragment (M-tile mo, K-step n), lane l: W[out unit qslot(16 mo + (l & 15))]
-// [in unit 4 n + (l >> 4)]; bias block: slot order, zero at padding slots.
+// A fragment (M-tile mo, K-step n), lane l: product output unit o = qslot(16 mo
+// + (l & 15)), input unit u = 4 n + (l >> 4): W[o][u] (forward) or W[u][o]
+// (transposed); bias block: slot order, zero at padding slots.
 __global__ void k_prepare_wide16(WPrep16 a, float* __restrict__ wreg) {
   const WSeg16& g = a.seg[blockIdx.x];
   const int64_t n = (int64_t)g.nm * g.nk * 64;
-  for (int64_t e = threadIdx.x; e < n; e += blockDim.x) {
+  const int c0 = g.first ? g.DT : 0;
+  for (int64_t e = threadIdx.x + (int64_t)blockIdx.y * blockDim.x; e < n;
+       e += (int64_t)blockDim.x * gridDim.y) {
     const int lane = (int)(e & 63), ks = (int)((e >> 6) % g.nk), mo = (int)((e >> 6) / g.nk);
     const int o = qslot(16 * mo + (lane & 15)), u = 4 * ks + (lane >> 4);
     float v = 0.f;
-    if (o < g.nout && u < g.nin) v = g.W[(int64_t)o * g.nin_full + (g.first ? g.DT : 0) + u];
+    if (o < g.nout && u < g.nin)
+      v = g.trans ? g.W[(int64_t)u * g.nin_full + c0 + o] : g.W[(int64_t)o * g.nin_full + c0 + u];
     wreg[g.adst + e] = v;
   }
+  if (g.bdst < 0 || blockIdx.y != 0) return;
   for (int s = threadIdx.x; s < 16 * g.nm; s += blockDim.x) {
     const int o = qslot(s);
     wreg[g.bdst + s] = o < g.nout ? g.b[o] : 0.f;
@@ -447,9 +1020,41 @@ struct WEntry16 {
   WFn fn[2][3];  // [nets - 1][forward, inverse, predict]
   int na, nb;    // A / bias floats per net and layer
   int ks[3], mt[3], abefore[3], bbefore[3];
+  TFwdFn tfwd[2];  // [nets - 1] training sweeps
+  TBwdFn tbwd[2];
+  int nat;         // transposed A floats per net and layer
+  int ksT[3], mtT[3], abeforeT[3];  // per reverse step i (forward Linear NL-1-i)
+  WTrain16Layout lay[2];  // [nets - 1]
 };
 
 #define CNF_G16(D, H1, H2) G16<D, H1, H2>
+#define CNF_G16T(D, H1, H2) G16T<D, H1, H2>
+
+template <int D, int H1, int H2, int NETS>
+constexpr WTrain16Layout train_layout() {
+  using TP = Tape16<D, H1, H2, NETS>;
+  using F = G16<D, H1, H2>;
+  WTrain16Layout y{};
+  y.RW = TP::RW;
+  y.GW = TP::GW;
+  y.xc = TP::XC;
+  y.cw = TP::CW;
+  y.xt = TP::XTo;
+  y.s = NETS == 2 ? TP::So : -1;
+  y.ts = TP::TS;
+  for (int n = 0; n < 2; ++n)
+    for (int k = 0; k < 3; ++k) {
+      const bool real = n < NETS && k >= 1 && k < F::NL;
+      y.h[n][k] = real ? TP::H(n, k) : -1;
+      y.gpre[n][k] = real ? TP::Gpre(n, k) : -1;
+    }
+  for (int k = 0; k < 3; ++k) {
+    y.hw[k] = k >= 1 && k < F::NL ? TP::HW(k) : 0;
+    y.gpw[k] = k >= 1 && k < F::NL ? TP::GP(k) : 0;
+  }
+  for (int n = 0; n < 2; ++n) y.glast[n] = n < NETS ? TP::Glast(n) : -1;
+  return y;
+}
 #define CNF_W16(D, H1, H2)                                                                    \
   {D, H1, H2,                                                                                 \
    {{k_wide16<D, H1, H2, 0, 1>, k_wide16<D, H1, H2, 1, 1>, k_wide16<D, H1, H2, 2, 1>},        \
@@ -460,7 +1065,15 @@ struct WEntry16 {
    {64 * CNF_G16(D, H1, H2)::sbefore(0), 64 * CNF_G16(D, H1, H2)::sbefore(1),                 \
     64 * CNF_G16(D, H1, H2)::sbefore(2)},                                                     \
    {CNF_G16(D, H1, H2)::bbefore(0), CNF_G16(D, H1, H2)::bbefore(1),                           \
-    CNF_G16(D, H1, H2)::bbefore(2)}}
+    CNF_G16(D, H1, H2)::bbefore(2)},                                                          \
+   {k_wtrain16_fwd<D, H1, H2, 1>, k_wtrain16_fwd<D, H1, H2, 2>},                              \
+   {k_wtrain16_bwd<D, H1, H2, 1>, k_wtrain16_bwd<D, H1, H2, 2>},                              \
+   CNF_G16T(D, H1, H2)::NA,                                                                   \
+   {CNF_G16T(D, H1, H2)::ks(0), CNF_G16T(D, H1, H2)::ks(1), CNF_G16T(D, H1, H2)::ks(2)},      \
+   {CNF_G16T(D, H1, H2)::mt(0), CNF_G16T(D, H1, H2)::mt(1), CNF_G16T(D, H1, H2)::mt(2)},      \
+   {64 * CNF_G16T(D, H1, H2)::sbefore(0), 64 * CNF_G16T(D, H1, H2)::sbefore(1),               \
+    64 * CNF_G16T(D, H1, H2)::sbefore(2)},                                                    \
+   {train_layout<D, H1, H2, 1>(), train_layout<D, H1, H2, 2>()}}
 
 const WEntry16 kW16Table[] = {
     CNF_W16(100, 100, 100),
@@ -481,9 +1094,11 @@ size_t w16_lds(const Shape& s) { return (size_t)kWaves * (kRows * (s.D | 1) + s.
 
 }  // namespace
 
+// per layer: the forward stream and biases (all layers first), then the
+// transposed stream of the reverse sweep (after the L forward records)
 int64_t wide16_layer_floats(const Shape& s) {
   const WEntry16* e = w16find(s);
-  return e ? (int64_t)(e->na + e->nb) * s.nets : 0;
+  return e ? (int64_t)(e->na + e->nb + e->nat) * s.nets : 0;
 }
 
 int wide16_prepare(const Shape& s, const float* const* params, void* prepared, hipStream_t st) {
@@ -492,6 +1107,7 @@ int wide16_prepare(const Shape& s, const float* const* params, void* prepared, h
   float* region = reinterpret_cast<float*>(static_cast<char*>(prepared) + idx_bytes(s)) +
                   s.wide_region;
   const int64_t LA = (int64_t)s.nets * e->na, LF = LA + (int64_t)s.nets * e->nb;
+  const int64_t LT = (int64_t)s.nets * e->nat;
   int pi = 0;
   for (int l = 0; l < s.L; ++l) {
     WPrep16 a{};
@@ -516,7 +1132,23 @@ int wide16_prepare(const Shape& s, const float* const* params, void* prepared, h
         g.bdst = (int64_t)l * LF + LA + (int64_t)pos * e->nb + e->bbefore[i];
       }
     }
-    hipLaunchKernelGGL(k_prepare_wide16, dim3(a.nseg), dim3(256), 0, st, a, region);
+    // the reverse sweep's stream: s-net first (natural net order), each net's
+    // Linears last first
+    for (int net = 0; net < s.nets; ++net)
+      for (int i = 0; i < s.n_lin; ++i) {
+        const WSeg16& f = a.seg[net * s.n_lin + i];
+        WSeg16& g = a.seg[a.nseg++];
+        g = f;
+        const int r = s.n_lin - 1 - i;  // reverse step of Linear i
+        g.trans = 1;
+        g.nin = f.nout;
+        g.nout = f.nin;
+        g.nm = e->mtT[r];
+        g.nk = e->ksT[r];
+        g.adst = (int64_t)s.L * LF + (int64_t)l * LT + (int64_t)net * e->nat + e->abeforeT[r];
+        g.bdst = -1;
+      }
+    hipLaunchKernelGGL(k_prepare_wide16, dim3(a.nseg, 8), dim3(256), 0, st, a, region);
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) {
       set_hip_error(err);
@@ -540,6 +1172,54 @@ int wide16_run(const Shape& s, const void* prepared, const float* in, float* out
   WFn fn = e->fn[s.nets - 1][log_priors ? 2 : (inverse ? 1 : 0)];
   hipLaunchKernelGGL(fn, grid, block, w16_lds(s), st, W, inverse ? inv_q : fwd_q, in, out, ld, B,
                      s.L, log_priors);
+  hipError_t err = hipGetLastError();
+  if (err != hipSuccess) {
+    set_hip_error(err);
+    return CNF_ERR_HIP;
+  }
+  return CNF_OK;
+}
+
+int wide16_train_layout(const Shape& s, WTrain16Layout* out) {
+  const WEntry16* e = w16find(s);
+  if (!e || s.nets < 1 || s.nets > 2) return CNF_ERR_UNSUPPORTED;
+  *out = e->lay[s.nets - 1];
+  return CNF_OK;
+}
+
+int wide16_train_forward(const Shape& s, const void* prepared, const float* x, float* zst, int Cp,
+                         int Dp, float* ld, float* tape, uint32_t* tbits, int64_t B,
+                         hipStream_t st) {
+  const WEntry16* e = w16find(s);
+  if (!e || s.nets < 1 || s.nets > 2) return CNF_ERR_UNSUPPORTED;
+  const char* base = static_cast<const char*>(prepared);
+  const int32_t* fwd_q = reinterpret_cast<const int32_t*>(base);
+  const float* W = reinterpret_cast<const float*>(base + idx_bytes(s)) + s.wide_region;
+  const int64_t rows_per_block = (int64_t)kRows * kWaves;
+  const dim3 grid((unsigned)((B + rows_per_block - 1) / rows_per_block)), block(64 * kWaves);
+  hipLaunchKernelGGL(e->tfwd[s.nets - 1], grid, block, w16_lds(s), st, W, fwd_q, x, zst, ld, tape,
+                     tbits, B, s.L, Cp, Dp);
+  hipError_t err = hipGetLastError();
+  if (err != hipSuccess) {
+    set_hip_error(err);
+    return CNF_ERR_HIP;
+  }
+  return CNF_OK;
+}
+
+int wide16_train_backward(const Shape& s, const void* prepared, const float* gz,
+                          const float* gz_all, float* dx, const float* gld, const float* tape,
+                          const uint32_t* tbits, float* gbuf, int64_t B, hipStream_t st) {
+  const WEntry16* e = w16find(s);
+  if (!e || s.nets < 1 || s.nets > 2) return CNF_ERR_UNSUPPORTED;
+  const char* base = static_cast<const char*>(prepared);
+  const int32_t* inv_q = reinterpret_cast<const int32_t*>(base) + s.L * s.D;
+  const float* W = reinterpret_cast<const float*>(base + idx_bytes(s)) + s.wide_region;
+  const int64_t LF = (int64_t)s.nets * (e->na + e->nb);
+  const int64_t rows_per_block = (int64_t)kRows * kWaves;
+  const dim3 grid((unsigned)((B + rows_per_block - 1) / rows_per_block)), block(64 * kWaves);
+  hipLaunchKernelGGL(e->tbwd[s.nets - 1], grid, block, w16_lds(s), st, W + s.L * LF, inv_q, gz,
+                     gz_all, dx, gld, tape, tbits, gbuf, B, s.L);
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) {
     set_hip_error(err);

@@ -325,6 +325,9 @@ struct DwJob {
   int cstep;           // +1, or -1 when the kernel's input columns run reversed (legacy)
   int rrev;            // output rows reversed (legacy): row n is parameter row N_full-1-n
   int nfull;
+  int gcl, hcl;        // last G / H column a lane may read (k_wdw16)
+  int slot;            // k_wdw16: G and H columns in slot order (the fused sweeps' layout:
+                       // column c holds unit slot_unit(c)), natural otherwise
 };
 struct DwArgs {
   DwJob job[2 * kMaxLin];
@@ -447,11 +450,31 @@ __global__ __launch_bounds__(256, 3) void k_wdw(DwArgs da) {
 // 49 tiles' MFMAs instead of 64, a cfg4 layer 18 % fewer in all.  Operand
 // loads per 16 rows are unchanged (K-step s: lane (i, q) reads G[row 4s + q]
 // [n + i] and H[row 4s + q][c + i], 64 contiguous bytes per quarter-wave).
-constexpr int kDw16CT = 7;  // 16-column tiles per wave (112 columns: [H | 1] of a 100-wide layer)
+#ifndef CNF_DW16_CT
+#define CNF_DW16_CT 7
+#endif
+// 16-column tiles per wave (7: 112 columns, [H | 1] of a 100-wide layer in one
+// block; 4: two blocks of 64 + 48 columns, half the accumulators, four waves
+// per SIMD)
+constexpr int kDw16CT = CNF_DW16_CT;
+#ifndef CNF_DW16_KS
+#define CNF_DW16_KS 4
+#endif
+// MFMA k-steps (of 4 rows) per operand set: 4 (16-row chunks, 149 VGPRs, 3
+// waves per SIMD) or 2 (8-row chunks, 4 waves per SIMD)
+constexpr int kDw16KS = CNF_DW16_KS;
 
-__global__ __launch_bounds__(256, 3) void k_wdw16(DwArgs da) {
+// unit of slot c in a 16-slot tile (cnf_wide16.hip's q-major fill; an involution)
+__device__ __forceinline__ int slot_unit(int c) {
+  return 16 * (c >> 4) + 4 * (c & 3) + ((c & 15) >> 2);
+}
+
+__global__ __launch_bounds__(256, (kDw16CT <= 4 || kDw16KS <= 2) ? 4 : 3) void k_wdw16(DwArgs da) {
   const DwJob j = da.job[blockIdx.y];
   const int lane = threadIdx.x & 63, i = lane & 15, kq = lane >> 4;
+  // (rotating the 32-row group a wave takes by the row block, to spread the
+  // short and idle waves of N = 100 / 50 jobs over the SIMDs, measured no
+  // change: 14.57 vs 14.60 ms per cfg4 step)
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int tiles16 = (j.K + 1 + 15) >> 4;
   const int nsub = (j.N + 31) >> 5, ncg = (tiles16 + kDw16CT - 1) / kDw16CT;
@@ -465,17 +488,40 @@ __global__ __launch_bounds__(256, 3) void k_wdw16(DwArgs da) {
   const int64_t r1 = min(da.M, r0 + da.rows);
   if (r0 >= r1) return;
   const int ldg = (int)j.ldg, ldh = (int)j.ldh;
+  // operand addressing.  Natural rows: element (r, c) at r * ld + c, k-step s
+  // 4 rows (4 ld floats) on.  Slot jobs read the fused sweeps' wave-tiled
+  // arrays (cnf_internal.h): (r, c) at (r >> 5) * 32 ld + (c >> 4) * 512 +
+  // ((r >> 4) & 1) * 256 + (r & 15) * 16 + (c & 15), k-step s 64 floats on
+  // (a 16-row chunk never leaves its row group).  Columns past a part clamp
+  // to its last column (tile).
   int goff[2], hoff[kDw16CT];
+  if (j.slot) {
 #pragma unroll
-  for (int t = 0; t < 2; ++t) goff[t] = (kq * ldg + min(n0 + 16 * t + i, j.N - 1)) * 4;
+    for (int t = 0; t < 2; ++t) goff[t] = (min((n0 >> 4) + t, j.gcl >> 4) * 512 + kq * 16 + i) * 4;
 #pragma unroll
-  for (int c = 0; c < kDw16CT; ++c) hoff[c] = (kq * ldh + min(c0 + 16 * c + i, ldh - 1)) * 4;
-  // 16-row chunks (4 MFMA k-steps of 4 rows) in two operand sets used in turn
-  constexpr int KS = 4;
+    for (int c = 0; c < kDw16CT; ++c)
+      hoff[c] = (min((c0 >> 4) + c, j.hcl >> 4) * 512 + kq * 16 + i) * 4;
+  } else {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) goff[t] = (kq * ldg + min(n0 + 16 * t + i, j.gcl)) * 4;
+#pragma unroll
+    for (int c = 0; c < kDw16CT; ++c) hoff[c] = (kq * ldh + min(c0 + 16 * c + i, j.hcl)) * 4;
+  }
+  const int gstep = j.slot ? 256 : 16 * ldg, hstep = j.slot ? 256 : 16 * ldh;  // bytes per k-step
+  auto chunk = [&](const float* P, int64_t ld, int64_t mr) {
+    return j.slot ? P + (mr >> 5) * 32 * ld + ((mr >> 4) & 1) * 256 + (mr & 15) * 16 : P + mr * ld;
+  };
+  auto elt = [&](const float* P, int64_t ld, int64_t r, int c, int cl) {
+    return j.slot ? P[(r >> 5) * 32 * ld + min(c >> 4, cl >> 4) * 512 + ((r >> 4) & 1) * 256 +
+                      (r & 15) * 16 + (c & 15)]
+                  : P[r * ld + min(c, cl)];
+  };
+  // chunks of 4 KS rows (KS MFMA k-steps of 4 rows) in two operand sets used in turn
+  constexpr int KS = kDw16KS, CH = 4 * KS;
   auto load = [&](int64_t mr, float (&a)[2][KS], float (&b)[kDw16CT][KS]) {
-    const auto gr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(j.G + mr * ldg), 0,
+    const auto gr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(chunk(j.G, ldg, mr)), 0,
                                                       0x7fffffff, 0x00020000);
-    const auto hr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(j.H + mr * ldh), 0,
+    const auto hr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(chunk(j.H, ldh, mr)), 0,
                                                       0x7fffffff, 0x00020000);
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -483,7 +529,7 @@ __global__ __launch_bounds__(256, 3) void k_wdw16(DwArgs da) {
 #pragma unroll
         for (int s = 0; s < KS; ++s)
           a[t][s] = __builtin_bit_cast(
-              float, __builtin_amdgcn_raw_buffer_load_b32(gr, goff[t], 4 * s * ldg * 4, 0));
+              float, __builtin_amdgcn_raw_buffer_load_b32(gr, goff[t], s * gstep, 0));
       }
 #pragma unroll
     for (int c = 0; c < kDw16CT; ++c)
@@ -491,39 +537,40 @@ __global__ __launch_bounds__(256, 3) void k_wdw16(DwArgs da) {
 #pragma unroll
         for (int s = 0; s < KS; ++s)
           b[c][s] = __builtin_bit_cast(
-              float, __builtin_amdgcn_raw_buffer_load_b32(hr, hoff[c], 4 * s * ldh * 4, 0));
+              float, __builtin_amdgcn_raw_buffer_load_b32(hr, hoff[c], s * hstep, 0));
       }
   };
+  // k-step outermost: consecutive MFMAs update different accumulators (a
+  // dependent 16x16x4 has 40 cycles of latency against 32 of issue)
   auto mfmas = [&](f4 (&acc)[2][kDw16CT], const float (*a)[KS], const float (*b)[KS]) {
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
-      if (t < nrs) {
+    for (int s = 0; s < KS; ++s)
 #pragma unroll
-        for (int c = 0; c < kDw16CT; ++c)
-          if (c < nct) {
+      for (int t = 0; t < 2; ++t)
+        if (t < nrs) {
 #pragma unroll
-            for (int s = 0; s < KS; ++s)
+          for (int c = 0; c < kDw16CT; ++c)
+            if (c < nct)
               acc[t][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][s], b[c][s], acc[t][c], 0, 0, 0);
-          }
-      }
+        }
   };
   f4 acc[2][kDw16CT];
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int c = 0; c < kDw16CT; ++c) acc[t][c] = f4{};
-  const int64_t rfull = r0 + (r1 - r0) / 16 * 16;  // rows in whole chunks
+  const int64_t rfull = r0 + (r1 - r0) / CH * CH;  // rows in whole chunks
   if (rfull > r0) {
     float a0[2][KS], b0[kDw16CT][KS], a1[2][KS], b1[kDw16CT][KS];
     load(r0, a0, b0);
-    for (int64_t mr = r0;; mr += 32) {
-      const bool more1 = mr + 16 < rfull;
-      if (more1) load(mr + 16, a1, b1);
+    for (int64_t mr = r0;; mr += 2 * CH) {
+      const bool more1 = mr + CH < rfull;
+      if (more1) load(mr + CH, a1, b1);
       __builtin_amdgcn_sched_barrier(0);
       mfmas(acc, a0, b0);
       if (!more1) break;
-      const bool more2 = mr + 32 < rfull;
-      if (more2) load(mr + 32, a0, b0);
+      const bool more2 = mr + 2 * CH < rfull;
+      if (more2) load(mr + 2 * CH, a0, b0);
       __builtin_amdgcn_sched_barrier(0);
       mfmas(acc, a1, b1);
       if (!more2) break;
@@ -537,24 +584,27 @@ __global__ __launch_bounds__(256, 3) void k_wdw16(DwArgs da) {
       const bool ok = row < r1;
       const int64_t rr = ok ? row : r1 - 1;
 #pragma unroll
-      for (int t = 0; t < 2; ++t) a[t][s] = ok ? j.G[rr * ldg + min(n0 + 16 * t + i, j.N - 1)] : 0.f;
+      for (int t = 0; t < 2; ++t) a[t][s] = ok ? elt(j.G, ldg, rr, n0 + 16 * t + i, j.gcl) : 0.f;
 #pragma unroll
-      for (int c = 0; c < kDw16CT; ++c) b[c][s] = j.H[rr * ldh + min(c0 + 16 * c + i, ldh - 1)];
+      for (int c = 0; c < kDw16CT; ++c) b[c][s] = elt(j.H, ldh, rr, c0 + 16 * c + i, j.hcl);
     }
     mfmas(acc, a, b);
   }
   // lane (i, kq), register q of tile (t, c): dW row n0 + 16 t + 4 kq + q, column c0 + 16 c + i
+  // (slot jobs: the units of those slots)
   float* out = da.partials + (int64_t)blockIdx.x * da.PS;
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     if (t >= nrs) continue;
 #pragma unroll
     for (int c = 0; c < kDw16CT; ++c) {
-      const int k = c0 + c * 16 + i;
+      const int kc = c0 + c * 16 + i;
+      const int k = j.slot ? slot_unit(kc) : kc;
       if (c >= nct || k > j.K) continue;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int nn = n0 + 16 * t + 4 * kq + q;
+        const int nc = n0 + 16 * t + 4 * kq + q;
+        const int nn = j.slot ? slot_unit(nc) : nc;
         if (nn >= j.N) continue;
         const int pr = j.rrev ? j.nfull - 1 - nn : nn;  // parameter row
         if (k < j.K) out[j.woff + (int64_t)pr * j.wld + (int64_t)j.cstep * k] = acc[t][c][q];
@@ -1119,8 +1169,130 @@ bool wvjp_ok(const Shape& s) {
   return gemm_lds(s.DC, lin_out(s, 0), s.nets == 2) <= kLds;
 }
 
+namespace {
+
+// ---- the fused training sweeps (cnf_wide16.hip: k_wtrain16_fwd / _bwd) ----
+// For the stacks k_wide16 serves, the layer-at-a-time GEMMs and update
+// kernels above give way to one forward launch (every layer, activations in
+// registers, a per-row tape written on the way) and one reverse launch per
+// layer; k_wseed and the weight-gradient launch (k_wdw16 on the slot-order
+// operands) stay.  Workspace: the tape of every layer (L x B x RW floats:
+// cfg4 at 2^18 rows 8.1 GB), the final output in the stash layout the seed
+// reads, ld / gld, two natural-order gradients, one layer's conditioner
+// gradients (B x GW), the seed and dW partials.
+struct Plan16 {
+  int64_t tape, tbits, zst, ld, gld, g0, gbuf, seed, part, total, nkb, rows_kb, nseed;
+};
+constexpr double kTapeMaxBytes = 96.0 * (1ull << 30);  // beyond: the layer-at-a-time path
+
+bool plan16(const Shape& s, int64_t B, WTrain16Layout* lay, Plan16* p) {
+  if (!wide16_train_ok(s) || wide16_train_layout(s, lay) != CNF_OK) return false;
+  const int64_t Bn = B > 0 ? B : 1;
+  const int64_t Bp = wide16_blocks(Bn) * 32;  // whole 32-row blocks (wave-tiled arrays)
+  if ((double)s.L * Bp * (lay->RW + lay->GW) * 4 > kTapeMaxBytes) return false;
+  const Geo g = geo(s);
+  int64_t off = 0;
+  auto take = [&](int64_t n) {
+    const int64_t o = off;
+    off += al64(n);
+    return o;
+  };
+  p->tape = take((int64_t)s.L * Bp * lay->RW);
+  p->tbits = take((int64_t)s.L * wide16_tbits_words(Bn));
+  p->zst = take(Bn * g.Dp);
+  p->ld = take(Bn);
+  p->gld = take(Bn);
+  p->g0 = take(Bn * s.D);
+  p->gbuf = take((int64_t)s.L * Bp * lay->GW);
+  p->nseed = std::min<int64_t>(4096, (Bn + 15) / 16);
+  p->seed = take(p->nseed * 4);
+  int64_t rows = (Bn + 255) / 256;
+  rows = std::max<int64_t>(256, (rows + 31) / 32 * 32);
+  p->rows_kb = rows;
+  p->nkb = (Bn + rows - 1) / rows;
+  p->part = take(p->nkb * al64(s.layer_floats));
+  p->total = off;
+  return true;
+}
+
+int wvjp16_run(const Shape& s, const WTrain16Layout& lay, const Plan16& p, const void* prepared,
+               const float* x, const int64_t* y, const float* gz, const float* gz_all,
+               const float* gld_in, int kind, float det, float grad_scale, float* loss_terms,
+               float* grads, float* dx, int64_t B, float* W, hipStream_t st) {
+  const Geo geom = geo(s);
+  const int D = s.D, L = s.L, NL = s.n_lin;
+  float* ld = W + p.ld;
+  float* gld = W + p.gld;
+  float* tape = W + p.tape;
+  uint32_t* tbits = reinterpret_cast<uint32_t*>(W + p.tbits);
+  int r = wide16_train_forward(s, prepared, x, W + p.zst, geom.Cp, geom.Dp, ld, tape, tbits, B, st);
+  if (r != CNF_OK) return r;
+  float* g[1] = {W + p.g0};
+  hipLaunchKernelGGL(k_wseed, dim3((unsigned)p.nseed), dim3(256), 0, st, W + p.zst, ld, y, kind,
+                     det, grad_scale, gz, gz_all ? gz_all + (int64_t)(L - 1) * B * D : nullptr,
+                     gld_in, g[0], gld, W + p.seed, B, geom);
+  if (kind >= 0) reduce_partials(W + p.seed, (int)p.nseed, 4, 0, nullptr, loss_terms, st);
+  const int64_t PL = s.layer_floats, PS = al64(PL);
+  float* part = W + p.part;
+  if (PL > 0 && hipMemsetAsync(part, 0, (size_t)p.nkb * PS * 4, st) != hipSuccess)
+    return check_launch();
+  r = wide16_train_backward(s, prepared, g[0], gz_all, dx, gld, tape, tbits, W + p.gbuf, B, st);
+  if (r != CNF_OK) return r;
+  const int64_t Bp = wide16_blocks(B) * 32;
+  for (int l = L - 1; l >= 0; --l) {
+    const float* tl = tape + (int64_t)l * Bp * lay.RW;
+    const float* gl = W + p.gbuf + (int64_t)l * Bp * lay.GW;
+    DwArgs da{};
+    da.partials = part;
+    da.M = B;
+    da.rows = p.rows_kb;
+    da.PS = PS;
+    int jobs = 0, max_subs = 1;
+    for (int n = 0; n < s.nets; ++n)
+      for (int k = 0; k < NL; ++k) {
+        DwJob& j = da.job[jobs++];
+        const bool last = k == NL - 1;
+        // wave-tiled parts: a part starting at column c begins (c / 16) * 512
+        // floats into each 32-row block
+        j.G = gl + (int64_t)(last ? lay.glast[n] : lay.gpre[n][k + 1]) / 16 * 512;
+        j.ldg = lay.GW;
+        j.gcl = (last ? lay.ts : lay.gpw[k + 1]) - 1;
+        j.H = tl + (int64_t)(k == 0 ? lay.xc : lay.h[n][k]) / 16 * 512;
+        j.ldh = lay.RW;
+        j.hcl = (k == 0 ? lay.cw : lay.hw[k]) - 1;
+        j.N = last ? s.DT : s.units[k + 1];
+        j.K = k == 0 ? s.DC : s.units[k];
+        j.slot = 1;
+        j.cstep = 1;
+        j.rrev = 0;
+        j.nfull = s.units[k + 1];
+        j.woff = n * s.net_floats + lin_off(s, k) + (k == 0 ? s.DT : 0);
+        j.wld = s.units[k];
+        j.boff = n * s.net_floats + lin_off(s, k) + (int64_t)s.units[k + 1] * s.units[k];
+        j.tiles_c = (j.K + 1 + 31) / 32;
+        const int ncg = ((j.K + 1 + 15) / 16 + kDw16CT - 1) / kDw16CT;
+        max_subs = std::max(max_subs, ((j.N + 127) / 128) * ncg);
+      }
+    hipLaunchKernelGGL(k_wdw16, dim3((unsigned)p.nkb, (unsigned)jobs, (unsigned)max_subs),
+                       dim3(256), 0, st, da);
+    reduce_partials(part, (int)p.nkb, (int)PS, (int)PL, grads + (int64_t)l * PL, nullptr, st);
+  }
+  return check_launch();
+}
+
+}  // namespace
+
 int wvjp_workspace(const Shape& s, int64_t B, size_t* bytes) {
   if (!wvjp_ok(s)) return CNF_ERR_UNSUPPORTED;
+  WTrain16Layout lay;
+  Plan16 p16;
+  *bytes = (size_t)(plan16(s, B, &lay, &p16) ? p16.total : make_plan(s, B).total) * 4;
+  return CNF_OK;
+}
+
+// the inverse transform's reverse mode always runs layer at a time
+int wvjp_inv_workspace(const Shape& s, int64_t B, size_t* bytes) {
+  if (!wvjp_ok(s) || s.strict) return CNF_ERR_UNSUPPORTED;
   *bytes = (size_t)make_plan(s, B).total * 4;
   return CNF_OK;
 }
@@ -1280,6 +1452,9 @@ struct Runner {
         j.wld = s.units[k];
         j.boff = n * s.net_floats + lin_off(s, k) + (int64_t)s.units[k + 1] * s.units[k];
         j.tiles_c = (j.K + 1 + 31) / 32;
+        j.gcl = j.N - 1;
+        j.hcl = (int)j.ldh - 1;
+        j.slot = 0;
         const int ncg = CNF_WDW16 ? ((j.K + 1 + 15) / 16 + kDw16CT - 1) / kDw16CT
                                   : (j.tiles_c + kDwCT - 1) / kDwCT;
         max_subs = std::max(max_subs, ((j.N + 127) / 128) * ncg);
@@ -1307,6 +1482,16 @@ int wvjp_run(const Shape& s, const void* prepared, const float* x, const int64_t
              float grad_scale, float* loss_terms, float* grads, float* dx, int64_t B, void* ws,
              size_t ws_bytes, hipStream_t st) {
   if (!wvjp_ok(s)) return CNF_ERR_UNSUPPORTED;
+  {
+    WTrain16Layout lay;
+    Plan16 p16;
+    if (plan16(s, B, &lay, &p16)) {
+      if (!ws || ws_bytes < (size_t)p16.total * 4) return CNF_ERR_NULL;
+      if (B == 0) return empty_batch(s, grads, loss_terms, st);
+      return wvjp16_run(s, lay, p16, prepared, x, y, gz, gz_all, gld_in, kind, det, grad_scale,
+                        loss_terms, grads, dx, B, static_cast<float*>(ws), st);
+    }
+  }
   const Plan p = make_plan(s, B);
   if (!ws || ws_bytes < (size_t)p.total * 4) return CNF_ERR_NULL;
   if (B == 0) return empty_batch(s, grads, loss_terms, st);
@@ -1369,6 +1554,7 @@ int wvjp_inv_run(const Shape& s, const void* prepared, const float* z, const flo
                  const float* gx_all, const float* gld_in, float* grads, float* dz, int64_t B,
                  void* ws, size_t ws_bytes, hipStream_t st) {
   if (!wvjp_ok(s) || s.strict) return CNF_ERR_UNSUPPORTED;  // strict: forward reverse mode only
+  // (the workspace is wvjp_inv_workspace's: the layer-at-a-time plan)
   const Plan p = make_plan(s, B);
   if (!ws || ws_bytes < (size_t)p.total * 4) return CNF_ERR_NULL;
   if (B == 0) return empty_batch(s, grads, nullptr, st);
