@@ -73,6 +73,7 @@ class CouplingStack:
         self._cache = {}
         self._loss_ws = {}
         self._vjp_ok = None
+        self._vjp_inv_ok = None
 
     # -- descriptor and permutations ----------------------------------------
     def _perm_tensors(self):
@@ -306,10 +307,29 @@ class CouplingStack:
         return _StackFn.apply(self, want_all, x, *ps)
 
 
+    def has_native_vjp_inverse(self):
+        """True when cnf_vjp_inverse serves this descriptor (not strict_nan)."""
+        if self._vjp_inv_ok is None:
+            n = ctypes.c_size_t()
+            st = _lib.lib().cnf_vjp_inverse_workspace_bytes(ctypes.byref(self.desc),
+                                                            ctypes.c_int64(1), ctypes.byref(n))
+            self._vjp_inv_ok = st == 0
+        return self._vjp_inv_ok
+
     def inverse_autograd(self, z, want_all):
         """Inverse with gradients w.r.t. z and every parameter
-        (cnf_vjp_inverse, the layer-at-a-time reverse mode)."""
-        return _InvStackFn.apply(self, want_all, z, *self.param_tensors())
+        (cnf_vjp_inverse, the layer-at-a-time reverse mode): the
+        cnf::inverse_flow operator (autograd kernel in C++) or the Python
+        Function."""
+        ps = self.param_tensors()
+        ops = _ops()
+        if ops is not None and self.has_native_vjp_inverse():
+            z = self._check_input(z)
+            blob = self.prepared(z.device)
+            stats["inverse"] += 1
+            stats["torch_ops"] += 1
+            return ops.inverse_flow(z, blob, self.desc_ints, self._perms, want_all, ps)
+        return _InvStackFn.apply(self, want_all, z, *ps)
 
 
 class _InvStackFn(torch.autograd.Function):

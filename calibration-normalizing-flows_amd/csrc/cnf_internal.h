@@ -120,10 +120,21 @@ struct WTrain16Layout {
 // (c & 15)); one array of a layer is wide16_blocks(B) * 32 * W floats.
 int wide16_train_layout(const Shape& s, WTrain16Layout* out);
 inline int64_t wide16_blocks(int64_t B) { return (B + 31) / 32; }
+// The loss seed fused into the forward sweep (null: the final output goes to
+// zst / ld for k_wseed): per row the gradient of z_L (G, [B][D]) and of ld
+// (gld), per 32-row wave the (loss, ce, ld) sums (part, 4 floats each).
+struct WSeed16 {
+  const int64_t* y;
+  float* G;
+  float* gld;
+  float* part;
+  float det, grad_scale;
+  int kind;
+};
 // tbits: relu' bits, 512 words per 32 rows and layer (wide16_tbits_words)
 int wide16_train_forward(const Shape& s, const void* prepared, const float* x, float* zst, int Cp,
                          int Dp, float* ld, float* tape, uint32_t* tbits, int64_t B,
-                         hipStream_t st);
+                         const WSeed16* seed, hipStream_t st);
 // the reverse sweep of every layer (one launch); gz: the seed (gradient of
 // the last output), gz_all: [L][B][D] or null, dx: or null; gbuf: L x B x GW
 int wide16_train_backward(const Shape& s, const void* prepared, const float* gz,

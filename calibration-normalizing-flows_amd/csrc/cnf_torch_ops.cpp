@@ -14,6 +14,10 @@
 //   cnf::loss_and_grads(x, y, prepared, desc, perms, kind, det, grad_scale) -> (terms, grads)
 //       fused training step                    calibrators.py:284-295
 //   cnf::vjp(x, prepared, desc, perms, gz, gz_all, gld, need_dx) -> (grads, dx)
+//   cnf::inverse_flow(z, prepared, desc, perms, all_outputs, params) -> (out, logdet)
+//       Flow.backward with gradients for z and every parameter (autograd;
+//       backward = cnf_vjp_inverse)            flows/flows.py:27-37, 114-126
+//   cnf::vjp_inverse(z, prepared, desc, perms, gx, gx_all, gld, need_dz) -> (grads, dz)
 //   cnf::predict(x, prepared, desc, perms, log_priors) -> probs
 //       Calibrator.predict                     calibrators.py:40-44, 330-353
 //
@@ -180,6 +184,34 @@ std::tuple<Tensor, Tensor> vjp_impl(const Tensor& x_, const Tensor& prepared,
   return {grads, dx};
 }
 
+std::tuple<Tensor, Tensor> vjp_inverse_impl(const Tensor& z_, const Tensor& prepared,
+                                            c10::IntArrayRef desc,
+                                            const c10::optional<Tensor>& perms,
+                                            const c10::optional<Tensor>& gx,
+                                            const c10::optional<Tensor>& gx_all,
+                                            const c10::optional<Tensor>& gld, bool need_dz) {
+  DevGuard guard(z_.device());
+  Desc d = make_desc(desc, perms);
+  Tensor z = rows(z_, d);
+  const int64_t B = z.size(0);
+  auto cont = [](const c10::optional<Tensor>& t) -> c10::optional<Tensor> {
+    if (!t.has_value() || !t->defined()) return c10::nullopt;
+    return t->to(torch::kFloat32).contiguous();
+  };
+  c10::optional<Tensor> g1 = cont(gx), g2 = cont(gx_all), g3 = cont(gld);
+  if (g3.has_value() && g3->numel() == 1 && B != 1) g3 = g3->reshape({1}).expand({B}).contiguous();
+  size_t n = 0;
+  check("cnf_vjp_inverse_workspace_bytes", cnf_vjp_inverse_workspace_bytes(&d.d, B, &n));
+  Tensor ws = torch::empty({(int64_t)std::max<size_t>(n, 16)}, z.options().dtype(torch::kUInt8));
+  Tensor grads = torch::empty({param_count(d)}, z.options());
+  Tensor dz = need_dz ? torch::empty_like(z) : Tensor();
+  check("cnf_vjp_inverse",
+        cnf_vjp_inverse(&d.d, prepared.data_ptr(), z.data_ptr<float>(), fptr(g1), fptr(g2),
+                        fptr(g3), grads.data_ptr<float>(), need_dz ? dz.data_ptr<float>() : nullptr,
+                        B, ws.data_ptr(), n, stream(z)));
+  return {grads, dz};
+}
+
 Tensor predict_impl(const Tensor& x_, const Tensor& prepared, c10::IntArrayRef desc,
                     const c10::optional<Tensor>& perms, const Tensor& log_priors) {
   DevGuard guard(x_.device());
@@ -195,14 +227,16 @@ Tensor predict_impl(const Tensor& x_, const Tensor& prepared, c10::IntArrayRef d
 }
 
 // Autograd: forward = one fused launch, backward = cnf_vjp (recomputes the
-// forward inside; nothing but x is saved).
-class FlowFn : public torch::autograd::Function<FlowFn> {
+// forward inside; nothing but x is saved).  INV: the inverse transform
+// (Flow.backward), backward = cnf_vjp_inverse.
+template <bool INV>
+class FlowFnT : public torch::autograd::Function<FlowFnT<INV>> {
  public:
   static variable_list forward(AutogradContext* ctx, const Tensor& x, const Tensor& prepared,
                                c10::IntArrayRef desc, const c10::optional<Tensor>& perms,
                                bool all_outputs, at::TensorList params) {
     at::AutoDispatchBelowADInplaceOrView guard;
-    auto [out, ld] = forward_impl(x, prepared, desc, perms, false, all_outputs);
+    auto [out, ld] = forward_impl(x, prepared, desc, perms, INV, all_outputs);
     ctx->save_for_backward({x, prepared});
     ctx->saved_data["desc"] = std::vector<int64_t>(desc.begin(), desc.end());
     ctx->saved_data["perms"] = perms.has_value() ? *perms : Tensor();
@@ -235,9 +269,9 @@ class FlowFn : public torch::autograd::Function<FlowFn> {
     c10::optional<Tensor> gz, gza, gld;
     if (g[0].defined()) (all ? gza : gz) = g[0];
     if (g[1].defined()) gld = g[1];
-    auto [grads, dx] = vjp_impl(x, prepared, desc,
-                                perms.defined() ? c10::optional<Tensor>(perms) : c10::nullopt,
-                                gz, gza, gld, need_dx);
+    const c10::optional<Tensor> pm = perms.defined() ? c10::optional<Tensor>(perms) : c10::nullopt;
+    auto [grads, dx] = INV ? vjp_inverse_impl(x, prepared, desc, pm, gz, gza, gld, need_dx)
+                           : vjp_impl(x, prepared, desc, pm, gz, gza, gld, need_dx);
     variable_list out{dx, Tensor(), Tensor(), Tensor(), Tensor()};
     // the flat gradient (state_dict order) split and shaped per parameter
     int64_t off = 0;
@@ -249,17 +283,19 @@ class FlowFn : public torch::autograd::Function<FlowFn> {
   }
 };
 
+template <bool INV>
 std::tuple<Tensor, Tensor> flow_autograd(const Tensor& x, const Tensor& prepared,
                                          c10::IntArrayRef desc, const c10::optional<Tensor>& perms,
                                          bool all_outputs, const std::vector<Tensor>& params) {
-  auto r = FlowFn::apply(x, prepared, desc, perms, all_outputs, at::TensorList(params));
+  auto r = FlowFnT<INV>::apply(x, prepared, desc, perms, all_outputs, at::TensorList(params));
   return {r[0], r[1]};
 }
 
+template <bool INV>
 std::tuple<Tensor, Tensor> flow_plain(const Tensor& x, const Tensor& prepared,
                                       c10::IntArrayRef desc, const c10::optional<Tensor>& perms,
                                       bool all_outputs, const std::vector<Tensor>&) {
-  return forward_impl(x, prepared, desc, perms, false, all_outputs);
+  return forward_impl(x, prepared, desc, perms, INV, all_outputs);
 }
 
 }  // namespace
@@ -277,15 +313,24 @@ TORCH_LIBRARY(cnf, m) {
         "Tensor? gld, bool need_dx) -> (Tensor, Tensor)");
   m.def("predict(Tensor x, Tensor prepared, int[] desc, Tensor? perms, Tensor log_priors) "
         "-> Tensor");
+  m.def("inverse_flow(Tensor z, Tensor prepared, int[] desc, Tensor? perms, bool all_outputs, "
+        "Tensor[] params) -> (Tensor, Tensor)");
+  m.def("vjp_inverse(Tensor z, Tensor prepared, int[] desc, Tensor? perms, Tensor? gx, "
+        "Tensor? gx_all, Tensor? gld, bool need_dz) -> (Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(cnf, CUDA, m) {
   m.impl("forward", forward_impl);
-  m.impl("flow", flow_plain);
+  m.impl("flow", flow_plain<false>);
+  m.impl("inverse_flow", flow_plain<true>);
+  m.impl("vjp_inverse", vjp_inverse_impl);
   m.impl("forward_loss", forward_loss_impl);
   m.impl("loss_and_grads", loss_and_grads_impl);
   m.impl("vjp", vjp_impl);
   m.impl("predict", predict_impl);
 }
 
-TORCH_LIBRARY_IMPL(cnf, Autograd, m) { m.impl("flow", flow_autograd); }
+TORCH_LIBRARY_IMPL(cnf, Autograd, m) {
+  m.impl("flow", flow_autograd<false>);
+  m.impl("inverse_flow", flow_autograd<true>);
+}

@@ -476,14 +476,15 @@ struct Tape16 {
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 
-// A/B knobs (never shipped changed): which tape traffic runs -- bit 0 the
+// A/B knobs: which tape traffic runs (never shipped changed) -- bit 0 the
 // XC / XT / S stores, 1 the hidden stores, 2 the reverse sweep's G stores --
-// and the stores' cache-policy bits
+// and the stores' cache-policy bits (nt measured 0.45 ms faster per forward
+// sweep and 0.36 ms per reverse sweep at cfg4 than default-policy stores)
 #ifndef CNF_W16_TAPE
 #define CNF_W16_TAPE 15
 #endif
 #ifndef CNF_W16_STORE_AUX
-#define CNF_W16_STORE_AUX 0
+#define CNF_W16_STORE_AUX 2  // nt: streaming stores (tape reuse is a whole sweep away)
 #endif
 
 // One wave's block of a wave-tiled [B][W] array (the tape and G layouts):
@@ -655,15 +656,83 @@ __device__ __forceinline__ void net_tape(float (&ring)[P], const float* __restri
   }
 }
 
+// The loss seed of a wave's 32 rows (z_L in LDS, natural order; the
+// calibrator NLL or CE of calibrators.py:287-291 / run_experiment3D.py:102-107,
+// as k_wseed in cnf_wvjp.hip): lane (r, h) = (lane & 31, lane >> 5) takes
+// half of row r's features.  Writes the gradient of z_L into the LDS rows,
+// gld per row, and the wave's (loss, ce, ld) sums to part[0..2] (fixed
+// order: deterministic).
+struct SeedArgs {
+  const int64_t* y;
+  float* G;     // [B][D] gradient of z_L
+  float* gld;   // [B]
+  float* part;  // [waves][4]
+  float det, grad_scale;
+  int kind;     // CNF_LOSS_*, or < 0: no seed (the final output goes to zst)
+};
+template <int D>
+__device__ __forceinline__ void row_seed(float* st, int S, int lane, int64_t row0, int nrows,
+                                         float ldr, const SeedArgs& a) {
+  constexpr int HF = (D + 1) / 2;
+  const int row = lane & 31, f0 = (lane >> 5) * HF, f1 = f0 + HF < D ? f0 + HF : D;
+  const bool valid = row < nrows;
+  float* r = st + row * S;
+  float m = -__builtin_inff();
+  for (int f = f0; f < f1; ++f) m = fmaxf(m, r[f]);
+  m = fmaxf(m, __shfl_xor(m, 32));
+  float se = 0.f;
+  for (int f = f0; f < f1; ++f) se += expf(r[f] - m);
+  se += __shfl_xor(se, 32);
+  const float lse = m + logf(se);
+  const int64_t yy = valid ? a.y[row0 + row] : 0;
+  const bool ok = yy >= 0 && yy < D;
+  const int yi = ok ? (int)yy : 0;
+  const float lpy = r[yi] - lse;
+  float coef, ce, loss, gl;
+  if (a.kind == CNF_LOSS_CAL) {  // -(log(softmax(z)[y] + 1e-7) + ld)
+    const float py = expf(lpy);
+    ce = -logf(py + 1e-7f);
+    loss = ce - ldr;
+    coef = py / (py + 1e-7f);
+    gl = -a.grad_scale;
+  } else {  // CE(z, y) - det * ld
+    ce = -lpy;
+    loss = ce - a.det * ldr;
+    coef = 1.f;
+    gl = -a.det * a.grad_scale;
+  }
+  if (!ok) ce = loss = coef = __builtin_nanf("");
+  wsync();  // every lane has read r[yi] before the row is overwritten
+  const float sc = a.grad_scale * coef;
+  for (int f = f0; f < f1; ++f) r[f] = sc * (expf(r[f] - lse) - (f == yi ? 1.f : 0.f));
+  if (valid && lane < 32) a.gld[row0 + row] = gl;
+  float s0 = valid && lane < 32 ? loss : 0.f, s1 = valid && lane < 32 ? ce : 0.f,
+        s2 = valid && lane < 32 ? ldr : 0.f;
+#pragma unroll
+  for (int o = 16; o >= 1; o >>= 1) {
+    s0 += __shfl_xor(s0, o);
+    s1 += __shfl_xor(s1, o);
+    s2 += __shfl_xor(s2, o);
+  }
+  if (lane == 0) {
+    float* p = a.part + (row0 / kRows) * 4;
+    p[0] = s0;
+    p[1] = s1;
+    p[2] = s2;
+    p[3] = 0.f;
+  }
+}
+
 // Forward sweep of training: k_wide16's forward with the tape of every layer
-// written on the way (stores interleaved with the MFMAs), the final output in
-// the stash layout the loss seed reads (column Cp + f for f < DT, f - DT
-// otherwise; row stride Dp) and each row's log-det.
+// written on the way, then either the loss seed (sa.kind >= 0: the gradient of
+// z_L, gld and the loss sums, as k_wseed) or the final output in the stash
+// layout k_wseed reads (column Cp + f for f < DT, f - DT otherwise; row stride
+// Dp) and each row's log-det.
 template <int D, int H1, int H2, int NETS>
 __global__ __launch_bounds__(64 * kWaves, 2) void k_wtrain16_fwd(
     const float* __restrict__ W, const int32_t* __restrict__ qtab, const float* __restrict__ in,
     float* __restrict__ zst, float* __restrict__ ld_out, float* __restrict__ tape,
-    uint32_t* __restrict__ tbits, int64_t B, int L, int Cp, int Dp) {
+    uint32_t* __restrict__ tbits, int64_t B, int L, int Cp, int Dp, SeedArgs sa) {
   using G = G16<D, H1, H2>;
   using TP = Tape16<D, H1, H2, NETS>;
   constexpr int XT = G::XT, CT = G::CT, TT = G::TT;
@@ -734,14 +803,25 @@ __global__ __launch_bounds__(64 * kWaves, 2) void k_wtrain16_fwd(
 
   put_state<G>(st, S, X, lane);
   wsync();
-  for (int i = lane; i < nrows * D; i += 64) {
-    const int r = i / D, f = i - r * D;
-    zst[(row0 + r) * Dp + (f < G::DT ? Cp + f : f - G::DT)] = st[r * S + f];
-  }
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
     ld[g] += __shfl_xor(ld[g], 16);
     ld[g] += __shfl_xor(ld[g], 32);
+  }
+  if (sa.kind >= 0) {
+    // lane l holds row (l & 15)'s log-det in ld[0] and row 16 + (l & 15)'s in ld[1]
+    row_seed<D>(st, S, lane, row0, nrows, (lane & 16) ? ld[1] : ld[0], sa);
+    wsync();
+    float* dst = sa.G + row0 * D;
+    for (int i = lane; i < nrows * D; i += 64) {
+      const int r = i / D, f = i - r * D;
+      dst[i] = st[r * S + f];
+    }
+    return;
+  }
+  for (int i = lane; i < nrows * D; i += 64) {
+    const int r = i / D, f = i - r * D;
+    zst[(row0 + r) * Dp + (f < G::DT ? Cp + f : f - G::DT)] = st[r * S + f];
   }
   if (lane < 16) {
 #pragma unroll
@@ -971,7 +1051,7 @@ __global__ __launch_bounds__(64 * kWaves, 2) void k_wtrain16_bwd(
 using WFn = void (*)(const float*, const int32_t*, const float*, float*, float*, int64_t, int,
                     const float*);
 using TFwdFn = void (*)(const float*, const int32_t*, const float*, float*, float*, float*,
-                        uint32_t*, int64_t, int, int, int);
+                        uint32_t*, int64_t, int, int, int, SeedArgs);
 using TBwdFn = void (*)(const float*, const int32_t*, const float*, const float*, float*,
                         const float*, const float*, const uint32_t*, float*, int64_t, int);
 
@@ -1189,7 +1269,7 @@ int wide16_train_layout(const Shape& s, WTrain16Layout* out) {
 
 int wide16_train_forward(const Shape& s, const void* prepared, const float* x, float* zst, int Cp,
                          int Dp, float* ld, float* tape, uint32_t* tbits, int64_t B,
-                         hipStream_t st) {
+                         const WSeed16* seed, hipStream_t st) {
   const WEntry16* e = w16find(s);
   if (!e || s.nets < 1 || s.nets > 2) return CNF_ERR_UNSUPPORTED;
   const char* base = static_cast<const char*>(prepared);
@@ -1197,8 +1277,19 @@ int wide16_train_forward(const Shape& s, const void* prepared, const float* x, f
   const float* W = reinterpret_cast<const float*>(base + idx_bytes(s)) + s.wide_region;
   const int64_t rows_per_block = (int64_t)kRows * kWaves;
   const dim3 grid((unsigned)((B + rows_per_block - 1) / rows_per_block)), block(64 * kWaves);
+  SeedArgs sa{};
+  sa.kind = -1;
+  if (seed) {
+    sa.y = seed->y;
+    sa.G = seed->G;
+    sa.gld = seed->gld;
+    sa.part = seed->part;
+    sa.det = seed->det;
+    sa.grad_scale = seed->grad_scale;
+    sa.kind = seed->kind;
+  }
   hipLaunchKernelGGL(e->tfwd[s.nets - 1], grid, block, w16_lds(s), st, W, fwd_q, x, zst, ld, tape,
-                     tbits, B, s.L, Cp, Dp);
+                     tbits, B, s.L, Cp, Dp, sa);
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) {
     set_hip_error(err);

@@ -1204,8 +1204,8 @@ bool plan16(const Shape& s, int64_t B, WTrain16Layout* lay, Plan16* p) {
   p->gld = take(Bn);
   p->g0 = take(Bn * s.D);
   p->gbuf = take((int64_t)s.L * Bp * lay->GW);
-  p->nseed = std::min<int64_t>(4096, (Bn + 15) / 16);
-  p->seed = take(p->nseed * 4);
+  p->nseed = std::min<int64_t>(4096, (Bn + 15) / 16);  // k_wseed's blocks (generic seeds)
+  p->seed = take(std::max<int64_t>(p->nseed, wide16_blocks(Bn)) * 4);  // or one record per wave
   int64_t rows = (Bn + 255) / 256;
   rows = std::max<int64_t>(256, (rows + 31) / 32 * 32);
   p->rows_kb = rows;
@@ -1225,18 +1225,26 @@ int wvjp16_run(const Shape& s, const WTrain16Layout& lay, const Plan16& p, const
   float* gld = W + p.gld;
   float* tape = W + p.tape;
   uint32_t* tbits = reinterpret_cast<uint32_t*>(W + p.tbits);
-  int r = wide16_train_forward(s, prepared, x, W + p.zst, geom.Cp, geom.Dp, ld, tape, tbits, B, st);
-  if (r != CNF_OK) return r;
   float* g[1] = {W + p.g0};
-  hipLaunchKernelGGL(k_wseed, dim3((unsigned)p.nseed), dim3(256), 0, st, W + p.zst, ld, y, kind,
-                     det, grad_scale, gz, gz_all ? gz_all + (int64_t)(L - 1) * B * D : nullptr,
-                     gld_in, g[0], gld, W + p.seed, B, geom);
-  if (kind >= 0) reduce_partials(W + p.seed, (int)p.nseed, 4, 0, nullptr, loss_terms, st);
+  if (kind >= 0) {  // the loss seed rides the forward sweep's epilogue
+    const WSeed16 sd{y, g[0], gld, W + p.seed, det, grad_scale, kind};
+    int r = wide16_train_forward(s, prepared, x, W + p.zst, geom.Cp, geom.Dp, ld, tape, tbits, B,
+                                 &sd, st);
+    if (r != CNF_OK) return r;
+    reduce_partials(W + p.seed, (int)wide16_blocks(B), 4, 0, nullptr, loss_terms, st);
+  } else {
+    int r = wide16_train_forward(s, prepared, x, W + p.zst, geom.Cp, geom.Dp, ld, tape, tbits, B,
+                                 nullptr, st);
+    if (r != CNF_OK) return r;
+    hipLaunchKernelGGL(k_wseed, dim3((unsigned)p.nseed), dim3(256), 0, st, W + p.zst, ld, y, kind,
+                       det, grad_scale, gz, gz_all ? gz_all + (int64_t)(L - 1) * B * D : nullptr,
+                       gld_in, g[0], gld, W + p.seed, B, geom);
+  }
   const int64_t PL = s.layer_floats, PS = al64(PL);
   float* part = W + p.part;
   if (PL > 0 && hipMemsetAsync(part, 0, (size_t)p.nkb * PS * 4, st) != hipSuccess)
     return check_launch();
-  r = wide16_train_backward(s, prepared, g[0], gz_all, dx, gld, tape, tbits, W + p.gbuf, B, st);
+  int r = wide16_train_backward(s, prepared, g[0], gz_all, dx, gld, tape, tbits, W + p.gbuf, B, st);
   if (r != CNF_OK) return r;
   const int64_t Bp = wide16_blocks(B) * 32;
   for (int l = L - 1; l >= 0; --l) {

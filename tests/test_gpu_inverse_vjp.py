@@ -42,7 +42,11 @@ def _err(a, b):
     (17, 3, [], True, True, False),       # odd D, no hidden layer
     (100, 2, [100, 100], True, True, True),
 ])
-def test_inverse_autograd_matches_cpu(D, L, hidden, scale, shift, flip):
+@pytest.mark.parametrize("via_ops", [True, False])
+def test_inverse_autograd_matches_cpu(D, L, hidden, scale, shift, flip, via_ops, monkeypatch):
+    # via_ops: the cnf::inverse_flow operator (C++ autograd kernel); else the
+    # Python autograd Function over ctypes
+    monkeypatch.setattr(engine, "USE_TORCH_OPS", via_ops)
     f = _flow(D, L, hidden, 0.1 if D <= 20 else 0.05, 3, scale, shift, flip)
     z = torch.randn(333, D, generator=torch.Generator().manual_seed(1))
     w = torch.randn(L, 333, D, generator=torch.Generator().manual_seed(2))
@@ -59,9 +63,13 @@ def test_inverse_autograd_matches_cpu(D, L, hidden, scale, shift, flip):
     fg = f.to(DEV)
     fg.zero_grad()
     zg = z.to(DEV).requires_grad_(True)
-    n0 = engine.stats["vjp"]
+    n0, t0 = engine.stats["vjp"], engine.stats["torch_ops"]
     objective(fg, zg).backward()
-    assert engine.stats["vjp"] == n0 + 1, "native cnf_vjp_inverse did not run"
+    if via_ops:
+        assert engine.stats["torch_ops"] == t0 + 1 and engine.stats["vjp"] == n0, \
+            "cnf::inverse_flow did not run"
+    else:
+        assert engine.stats["vjp"] == n0 + 1, "native cnf_vjp_inverse did not run"
     for k, p in fg.named_parameters():
         if p.requires_grad:
             assert _err(p.grad.cpu(), ref[k]) <= 1e-4, k
