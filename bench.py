@@ -162,7 +162,7 @@ class Runner:
 
     def kernel_symbol(self):
         return {"valu-fused": "k_valu", "sgpr-fused": "k_sgpr", "mfma-tile": "k_tile",
-                "mfma-wide": "k_wide"}.get(
+                "mfma-wide": "k_wide16"}.get(
             self.stack.kernel_name(), self.stack.kernel_name())
 
     def step(self):

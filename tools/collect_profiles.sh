@@ -11,12 +11,13 @@ for d in gpurun_out/prof_${TAG}_*; do
   n=${d#gpurun_out/prof_${TAG}_}
   [ -f $d/run_kernel_stats.csv ] && cp $d/run_kernel_stats.csv profiles/${TAG}_${n}_kernel_stats.csv
 done
-for spec in "cfg2 loss k_sgpr 1048576" "cfg2 all k_valu 1048576" "cfg2 train k_vjp2 1048576" "cfg4 forward k_wide 262144" "cfg4 train k_wdw 262144"; do
+for spec in "cfg2 loss k_sgpr 1048576" "cfg2 all k_valu 1048576" "cfg2 train k_vjp2 1048576" "cfg4 forward k_wide16 262144" "cfg4 train k_wdw16 262144" "cfg4 train k_wtrain16_fwd 262144" "cfg4 train k_wtrain16_bwd 262144"; do
   set -- $spec
   dir=gpurun_out/pmc_${TAG}_$1_$2_$1
   [ -d $dir ] || continue
-  python tools/pmc_summary.py $dir $3 > profiles/${TAG}_pmc_$1_$2.txt
-  python tools/pmc_traffic.py $dir profiles/${TAG}_traffic_$1_$2.json $1 $4 $3 > /dev/null
+  sfx=$1_$2; case "$3" in k_wtrain16*) sfx=$1_$2_$3;; esac
+  python tools/pmc_summary.py $dir $3 > profiles/${TAG}_pmc_${sfx}.txt
+  python tools/pmc_traffic.py $dir profiles/${TAG}_traffic_${sfx}.json $1 $4 $3 > /dev/null
 done
 grep '^{"metric"' gpurun_out/bench.log | tail -1 >> profiles/${TAG}_bench.jsonl
 ls profiles/ | grep "^${TAG}_"

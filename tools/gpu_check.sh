@@ -32,12 +32,16 @@ done
 # PMC passes: HBM traffic (separate FETCH / WRITE passes) and issue counters
 VALU="SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM GRBM_GUI_ACTIVE"
 MFMA="SQ_WAVES SQ_INSTS_VALU_MFMA_F32 SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE"
-for spec in "cfg2 loss k_sgpr" "cfg2 all k_valu" "cfg2 train k_vjp2" "cfg4 forward k_wide" "cfg4 train k_wdw"; do
+for spec in "cfg2 loss k_sgpr" "cfg2 all k_valu" "cfg2 train k_vjp2" "cfg4 forward k_wide16" "cfg4 train k_wdw16"; do
   set -- $spec
   rm -rf gpurun_out/pmc_${TAG}_$1_$2_$1
-  CTR="$VALU"; case "$3" in k_wide|k_vjp2|k_wdw) CTR="$MFMA";; esac
+  CTR="$VALU"; case "$3" in k_wide*|k_vjp2|k_wdw*) CTR="$MFMA";; esac
   NL=20; [ "$1 $2" = "cfg4 train" ] && NL=2
   run pmc_$1_$2 600 bash tools/gpu_pmc.sh ${TAG}_$1_$2 $1 "--mode $2 --launches $NL" "FETCH_SIZE" "WRITE_SIZE" "$CTR"
   python tools/pmc_summary.py gpurun_out/pmc_${TAG}_$1_$2_$1 $3 > gpurun_out/${TAG}_pmc_$1_$2.txt 2>&1
+done
+# the fused wide training sweeps, from the cfg4 train pass
+for k in k_wtrain16_fwd k_wtrain16_bwd; do
+  python tools/pmc_summary.py gpurun_out/pmc_${TAG}_cfg4_train_cfg4 $k > gpurun_out/${TAG}_pmc_cfg4_train_$k.txt 2>&1
 done
 exit 0
