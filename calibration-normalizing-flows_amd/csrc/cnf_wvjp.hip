@@ -614,8 +614,120 @@ __global__ __launch_bounds__(256, (kDw16CT <= 4 || kDw16KS <= 2) ? 4 : 3) void k
   }
 }
 
+// The fused sweeps' weight gradients (slot jobs on the wave-tiled G / H
+// arrays, cnf_internal.h) with each 32-row block's operand tiles staged in LDS:
+// in the wave-tiled layout a block's G part and H part are contiguous runs of
+// 2 KiB tiles, so the four waves copy them by LDS-DMA (global_load_lds, 1 KiB
+// per wave-instruction, no registers) into one of two stages while computing
+// the other, and every wave reads its MFMA operands from LDS -- H once per
+// block instead of once per wave.  Wave w takes the job's row tiles w and
+// w + 4 (of 7 for N = 100, of 4 for N = 50) over every column tile.  Rows past
+// the batch inside the last 32-row block are padding the sweeps wrote with
+// exact zeros in G (zero upstream gradients), so whole blocks are summed.
+// Compile-time tile counts (NTG G tiles, NTH H tiles, NR row tiles for this
+// wave), so the k-step body is straight-line MFMAs on LDS operands.
+template <int NTG, int NTH, int NR>
+__device__ __forceinline__ void wdwg_chunks(const DwJob& j, float* sm, int w, int lane, int64_t r0,
+                                            int nch, f4 (&acc)[2][8]) {
+  constexpr int TPC = NTG + NTH;
+  const int64_t ldg = j.ldg, ldh = j.ldh;
+  auto dma = [&](int c, int stg) {
+    const float* gsrc = j.G + ((r0 >> 5) + c) * 32 * ldg;
+    const float* hsrc = j.H + ((r0 >> 5) + c) * 32 * ldh;
+    float* dst = sm + stg * TPC * 512;
+#pragma unroll
+    for (int k0 = 0; k0 < 2 * TPC; k0 += 4) {  // 1 KiB pieces; piece k0 + w is this wave's
+      const int k = k0 + w;
+      if (k < 2 * TPC) {
+        const float* src = k < 2 * NTG ? gsrc + k * 256 : hsrc + (k - 2 * NTG) * 256;
+        __builtin_amdgcn_global_load_lds(const_cast<float*>(src) + lane * 4, dst + k * 256, 16, 0, 0);
+      }
+    }
+  };
+  dma(0, 0);
+  for (int c = 0; c < nch; ++c) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of chunk c
+    __syncthreads();  // everyone's pieces landed; everyone is done with chunk c - 1
+    if (c + 1 < nch) dma(c + 1, (c + 1) & 1);
+    const float* S = sm + (c & 1) * TPC * 512 + lane;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {  // 4 rows per k-step: row 4s + kq of the 32-row block
+      float a[NR > 0 ? NR : 1], b[NTH];
+#pragma unroll
+      for (int t = 0; t < NR; ++t) a[t] = S[(w + 4 * t) * 512 + s * 64];
+#pragma unroll
+      for (int q = 0; q < NTH; ++q) b[q] = S[(NTG + q) * 512 + s * 64];
+#pragma unroll
+      for (int t = 0; t < NR; ++t)
+#pragma unroll
+        for (int q = 0; q < NTH; ++q)
+          acc[t][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t], b[q], acc[t][q], 0, 0, 0);
+    }
+  }
+}
+
+// the (G tiles, H tiles) classes with an instantiation: the weight gradients
+// of k_wide16's table (cfg4: (7, 4), (7, 7), (4, 7))
+#define CNF_WDWG_CLASSES(X) X(7, 4) X(7, 7) X(4, 7) X(4, 4) X(4, 2) X(4, 5) X(1, 5)
+inline bool wdwg_class_ok(int ntg, int nth) {
+#define CNF_WDWG_OK(A, B) if (ntg == A && nth == B) return true;
+  CNF_WDWG_CLASSES(CNF_WDWG_OK)
+#undef CNF_WDWG_OK
+  return false;
+}
+
+__global__ __launch_bounds__(256, 2) void k_wdw16g(DwArgs da) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const DwJob j = da.job[blockIdx.y];
+  const int lane = threadIdx.x & 63, i = lane & 15, kq = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ntg = (j.gcl >> 4) + 1, nth = (j.hcl >> 4) + 1;
+  const int64_t r0 = (int64_t)blockIdx.x * da.rows;
+  const int64_t r1 = min(da.M, r0 + da.rows);  // da.M: the batch rounded up to 32
+  if (r0 >= r1) return;  // the whole block: no barrier reached
+  const int nch = (int)((r1 - r0) >> 5);
+  const int nr = (w < ntg ? 1 : 0) + (w + 4 < ntg ? 1 : 0);
+  f4 acc[2][8];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) acc[t][c] = f4{};
+  // every wave runs the chunk loop (it copies its share and meets the
+  // barriers) whatever its row-tile count
+#define CNF_WDWG_RUN(A, B)                                                    \
+  if (ntg == A && nth == B) {                                                 \
+    if (nr == 2) wdwg_chunks<A, B, 2>(j, sm, w, lane, r0, nch, acc);           \
+    else if (nr == 1) wdwg_chunks<A, B, 1>(j, sm, w, lane, r0, nch, acc);      \
+    else wdwg_chunks<A, B, 0>(j, sm, w, lane, r0, nch, acc);                   \
+  } else
+  CNF_WDWG_CLASSES(CNF_WDWG_RUN) {}
+#undef CNF_WDWG_RUN
+  // lane (i, kq), register q of tile (t, c): dW row slot 16 (w + 4t) + 4 kq + q,
+  // column slot 16 c + i, each mapped to its unit
+  float* out = da.partials + (int64_t)blockIdx.x * da.PS;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    if (t >= nr) continue;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int k = slot_unit(16 * c + i);
+      if (c >= nth || k > j.K) continue;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int nn = slot_unit(16 * (w + 4 * t) + 4 * kq + q);
+        if (nn >= j.N) continue;
+        if (k < j.K) out[j.woff + (int64_t)nn * j.wld + k] = acc[t][c][q];
+        else out[j.boff + nn] = acc[t][c][q];
+      }
+    }
+  }
+}
+
 #ifndef CNF_WDW16
 #define CNF_WDW16 1  // A/B: 0 keeps the 32x32 tiles of k_wdw
+#endif
+#ifndef CNF_WDW16G
+#define CNF_WDW16G 1  // A/B: 0 runs the fused sweeps' weight gradients on k_wdw16
 #endif
 
 __device__ __forceinline__ float wave_sum(float v) {
@@ -1281,8 +1393,21 @@ int wvjp16_run(const Shape& s, const WTrain16Layout& lay, const Plan16& p, const
         const int ncg = ((j.K + 1 + 15) / 16 + kDw16CT - 1) / kDw16CT;
         max_subs = std::max(max_subs, ((j.N + 127) / 128) * ncg);
       }
-    hipLaunchKernelGGL(k_wdw16, dim3((unsigned)p.nkb, (unsigned)jobs, (unsigned)max_subs),
-                       dim3(256), 0, st, da);
+    int maxtpc = 0;
+    bool gok = CNF_WDW16G;
+    for (int q = 0; q < jobs; ++q) {
+      const int ng = (da.job[q].gcl >> 4) + 1, nh = (da.job[q].hcl >> 4) + 1;
+      gok = gok && wdwg_class_ok(ng, nh);
+      maxtpc = std::max(maxtpc, ng + nh);
+    }
+    if (gok) {  // whole 32-row blocks (padding rows carry zero G)
+      da.M = Bp;
+      hipLaunchKernelGGL(k_wdw16g, dim3((unsigned)p.nkb, (unsigned)jobs), dim3(256),
+                         (size_t)2 * maxtpc * 2048, st, da);
+    } else {
+      hipLaunchKernelGGL(k_wdw16, dim3((unsigned)p.nkb, (unsigned)jobs, (unsigned)max_subs),
+                         dim3(256), 0, st, da);
+    }
     reduce_partials(part, (int)p.nkb, (int)PS, (int)PL, grads + (int64_t)l * PL, nullptr, st);
   }
   return check_launch();
