@@ -184,6 +184,21 @@ class Runner:
         if st != 0:
             raise RuntimeError("cnf launch failed: %d" % st)
 
+    def settle(self, seconds):
+        """Untimed steps until the device has run for `seconds` (the clock ramp
+        and first touch of the rotating sets: a 2^20-row loss step measured
+        36.3 us right after 20 warmup steps and 32.0 us once settled); returns
+        the number of steps run."""
+        n = 0
+        t0 = time.perf_counter()
+        while True:
+            for _ in range(32):
+                self.step()
+            n += 32
+            torch.cuda.synchronize(self.dev)
+            if time.perf_counter() - t0 >= seconds:
+                return n
+
     def timed(self, steps, warmup, collective=None):
         for _ in range(warmup):
             self.step()
@@ -441,6 +456,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--settle-s", type=float, default=0.3,
+                    help="untimed steps for this many seconds before the warmup (clock ramp)")
     ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
     ap.add_argument("--batch", type=int, default=0, help="vectors per GPU (default: config)")
     ap.add_argument("--rotate-gb", type=float, default=1.0)
@@ -496,6 +513,7 @@ def main():
         # NLL all-reduce over xGMI (configs[2]), overlapped with the next batch
         collective = NllAllReduce(runner, overlap=args.overlap_allreduce)
 
+    settle_steps = runner.settle(args.settle_s) if args.settle_s > 0 else 0
     t_dev, wall = runner.timed(args.steps, args.warmup, collective)
     sync_ms = None
     if args.dist_check:
@@ -568,6 +586,8 @@ def main():
             "value": round(value, 1),
             "unit": "logit-vectors/sec",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            # untimed steps before the warmup, until the device has run this long
+            "settle": {"seconds": args.settle_s, "steps": settle_steps},
             "ms_per_step": round(t_max / args.steps * 1e3, 5),
             # the rank count the process group reports, and each rank's own
             # ms/step (ms_per_step above is their max)

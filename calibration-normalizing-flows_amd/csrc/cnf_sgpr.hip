@@ -132,7 +132,7 @@ template <bool ALL, bool PERM>
 constexpr int pairs_per_lane() { return (ALL || PERM) ? 1 : CNF_SGPR_PAIRS; }
 // register budget (resident waves per SIMD) for a lane of P pairs
 #ifndef CNF_SGPR_WPS  // A/B builds: -DCNF_SGPR_WPS=n for the unpermuted one-pair variants
-#define CNF_SGPR_WPS 5
+#define CNF_SGPR_WPS 6
 #endif
 template <int MODE, bool ALL, bool PERM>
 constexpr int waves_per_simd() {
@@ -744,9 +744,12 @@ int resident_blocks(const KV& k, size_t lds) {
     n = 1;
   // at most CNF_SGPR_GRID_WPS blocks per CU even where the occupancy query
   // allows more: at 7 per CU (forward, 71 VGPRs) the last ~10 % of a 2^20-row
-  // grid was not resident at launch and started ~18 us late (tools/sgpr_trace.py)
+  // grid was not resident at launch and started ~18 us late (tools/sgpr_trace.py).
+  // 6 (with the 6-wave register budget, 80 VGPRs, no scratch) measured 0.6-0.8 us
+  // faster per 2^20-row loss / forward call than 5 (round 4, two interleaved
+  // A/B passes); 7 spills the loss build
 #ifndef CNF_SGPR_GRID_WPS
-#define CNF_SGPR_GRID_WPS 5
+#define CNF_SGPR_GRID_WPS 6
 #endif
   if (n > CNF_SGPR_GRID_WPS) n = CNF_SGPR_GRID_WPS;
   if (hipGetDevice(&dev) != hipSuccess ||
