@@ -48,6 +48,12 @@ typedef float v4 __attribute__((ext_vector_type(4)));
 #ifndef CNF_W16_PMAX
 #define CNF_W16_PMAX 16  // deepest A-operand ring
 #endif
+#ifndef CNF_W16_FWD_P16
+#define CNF_W16_FWD_P16 0  // the same for the forward streams: measured no change (2545 vs 2547 us cfg4 forward), spills the training forward; off
+#endif
+#ifndef CNF_W16_BWD_P16
+#define CNF_W16_BWD_P16 1  // pad the reverse stream per layer to 16-step multiples
+#endif
 
 constexpr int kRows = 32;   // rows per wave (two row groups of 16)
 constexpr int kWaves = 4;   // waves per block
@@ -77,6 +83,10 @@ struct G16 {
   static constexpr int bbefore(int i) { return i == 0 ? 0 : bbefore(i - 1) + 16 * mt(i - 1); }
   static constexpr int NA = steps() * 64;  // A-stream floats per net and layer
   static constexpr int NB = bbefore(NL);   // bias floats per net and layer
+  // A-stream steps per layer: padded to a multiple of 16 (a few fragments no
+  // MFMA uses) so the ring can be 16 deep (G16T below)
+  template <int NETS>
+  static constexpr int lsp() { return CNF_W16_FWD_P16 ? cdiv(NETS * steps(), 16) * 16 : NETS * steps(); }
   static constexpr int T1 = H1 > 0 ? cdiv(H1, 16) : 1, T2 = H2 > 0 ? cdiv(H2, 16) : 1;
 };
 
@@ -112,7 +122,7 @@ __device__ __forceinline__ void wsync() {
 template <class G, int NETS, int NET, int I, int MO, int N, int TOFF, int P, int TIN>
 __device__ __forceinline__ void kstep(v4 (&acc)[2], float (&ring)[P], const float* __restrict__ a,
                                       const float* __restrict__ an, const v4 (&in)[TIN][2]) {
-  constexpr int LS = NETS * G::steps();
+  constexpr int LS = G::template lsp<NETS>();  // stream steps per layer (pads included)
   constexpr int T = NET * G::steps() + G::sbefore(I) + MO * G::ks(I) + N;
   const float av = ring[T % P];
   if constexpr (T + P < LS) ring[T % P] = a[(T + P) * 64];
@@ -123,6 +133,22 @@ __device__ __forceinline__ void kstep(v4 (&acc)[2], float (&ring)[P], const floa
   // keep each refill where it is (left alone, the scheduler sinks the loads
   // next to their use and every MFMA waits for memory)
   __builtin_amdgcn_sched_barrier(0);
+}
+
+// the ring's refills for the stream's pad steps (no MFMA)
+template <class G, int NETS, int P, int T>
+__device__ __forceinline__ void pad_step(float (&ring)[P], const float* __restrict__ a,
+                                         const float* __restrict__ an) {
+  constexpr int LS = G::template lsp<NETS>();
+  if constexpr (T + P < LS) ring[T % P] = a[(T + P) * 64];
+  else ring[T % P] = an[(T + P - LS) * 64];
+  __builtin_amdgcn_sched_barrier(0);
+}
+template <class G, int NETS, int P, int... K>
+__device__ __forceinline__ void pad_steps(float (&ring)[P], const float* __restrict__ a,
+                                          const float* __restrict__ an,
+                                          std::integer_sequence<int, K...>) {
+  (pad_step<G, NETS, P, NETS * G::steps() + K>(ring, a, an), ...);
 }
 
 // Epilogues of an M-tile's accumulators: hidden (ReLU), keep (the t-net's
@@ -335,7 +361,8 @@ __global__ __launch_bounds__(64 * kWaves, 2) void k_wide16(
   constexpr bool INV = MODE == 1;
   constexpr int XT = G::XT, CT = G::CT, TT = G::TT;
   constexpr int S = D | 1;  // odd LDS row stride
-  constexpr int LA = NETS * G::NA, LF = LA + NETS * G::NB;  // A floats / all floats per layer
+  constexpr int LSP = G::template lsp<NETS>();
+  constexpr int LA = LSP * 64, LF = LA + NETS * G::NB;  // A floats / all floats per layer
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // SGPR: row0, descriptors
@@ -361,7 +388,7 @@ __global__ __launch_bounds__(64 * kWaves, 2) void k_wide16(
   wsync();
 
   // the A stream: one ring for the whole launch, P fragments ahead of the MFMAs
-  constexpr int P = ring16(NETS * G::steps(), CNF_W16_PMAX);
+  constexpr int P = ring16(LSP, CNF_W16_PMAX);
   float ring[P];
   {
     const float* a0 = W + (int64_t)(INV ? L - 1 : 0) * LF + lane;
@@ -390,6 +417,7 @@ __global__ __launch_bounds__(64 * kWaves, 2) void k_wide16(
 #pragma unroll
         for (int g = 0; g < 2; ++g) X[CT + t][g] = INV ? X[CT + t][g] - Tv[t][g] : X[CT + t][g] + Tv[t][g];
     }
+    pad_steps<G, NETS, P>(ring, wl, wn, std::make_integer_sequence<int, LSP - NETS * G::steps()>{});
     if constexpr (!INV) relayout<G>(st, qs, S, q, X, lane);  // perm then flip
   }
 
@@ -444,7 +472,14 @@ struct G16T {
   static constexpr int steps() { return sbefore(NL); }
   static constexpr int bbefore(int) { return 0; }
   static constexpr int NA = steps() * 64;
+  // The reverse sweep's stream per layer is padded to a multiple of 16 steps
+  // (a few fragments no MFMA uses): the A ring, which must divide the layer's
+  // steps, can then be 16 deep instead of 12, and every tape / G access gets 16
+  // K-steps to complete before a ring wait covers it (vmcnt counts in order).
+  template <int NETS>
+  static constexpr int lsp() { return CNF_W16_BWD_P16 ? cdiv(NETS * steps(), 16) * 16 : NETS * steps(); }
 };
+
 
 // Per-row tape of one layer, every part in slot order (16-slot tiles), so the
 // reverse sweep reads back exactly the register tiles the forward held:
@@ -737,7 +772,8 @@ __global__ __launch_bounds__(64 * kWaves, 2) void k_wtrain16_fwd(
   using TP = Tape16<D, H1, H2, NETS>;
   constexpr int XT = G::XT, CT = G::CT, TT = G::TT;
   constexpr int S = D | 1;
-  constexpr int LA = NETS * G::NA, LF = LA + NETS * G::NB;
+  constexpr int LSP = G::template lsp<NETS>();
+  constexpr int LA = LSP * 64, LF = LA + NETS * G::NB;
   constexpr int OC = qslot(G::DC);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int lane = threadIdx.x & 63;
@@ -759,7 +795,7 @@ __global__ __launch_bounds__(64 * kWaves, 2) void k_wtrain16_fwd(
   get_state<G>(st, S, nullptr, X, lane);
   wsync();
 
-  constexpr int P = ring16(NETS * G::steps(), CNF_W16_PMAX);
+  constexpr int P = ring16(LSP, CNF_W16_PMAX);
   float ring[P];
 #pragma unroll
   for (int j = 0; j < P; ++j) ring[j] = W[lane + j * 64];
@@ -798,6 +834,7 @@ __global__ __launch_bounds__(64 * kWaves, 2) void k_wtrain16_fwd(
 #pragma unroll
         for (int g = 0; g < 2; ++g) X[CT + t][g] = X[CT + t][g] + Tv[t][g];
     }
+    pad_steps<G, NETS, P>(ring, wl, wn, std::make_integer_sequence<int, LSP - NETS * G::steps()>{});
     relayout<G>(st, qs, S, qtab + l * D, X, lane);
   }
 
@@ -928,7 +965,8 @@ __global__ __launch_bounds__(64 * kWaves, 2) void k_wtrain16_bwd(
   using TP = Tape16<D, H1, H2, NETS>;
   constexpr int XT = G::XT, CT = G::CT, TT = G::TT;
   constexpr int S = D | 1;
-  constexpr int LT = NETS * GT::NA;  // transposed-stream floats per layer
+  constexpr int LSP = GT::template lsp<NETS>();
+  constexpr int LT = LSP * 64;  // transposed-stream floats per layer (pads included)
   constexpr float kL2E = 1.4426950408889634f;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int lane = threadIdx.x & 63;
@@ -945,7 +983,7 @@ __global__ __launch_bounds__(64 * kWaves, 2) void k_wtrain16_bwd(
     const int r = i / D, f = i - r * D;
     st[r * S + f] = r < nrows ? src[i] : 0.f;
   }
-  constexpr int P = ring16(NETS * GT::steps(), CNF_W16_PMAX);
+  constexpr int P = ring16(LSP, CNF_W16_PMAX);
   float ring[P];
   {
     const float* a0 = WT + (int64_t)(L - 1) * LT + lane;
@@ -1033,6 +1071,7 @@ __global__ __launch_bounds__(64 * kWaves, 2) void k_wtrain16_bwd(
         for (int g = 0; g < 2; ++g) gb.store(X[CT + t][g], g, TP::Glast(0) + 16 * t);
       net_back<GT, TP, 1, 0, CT>(ring, wa, wn, X, X, mb, gb, lane);
     }
+    pad_steps<GT, NETS, P>(ring, wa, wn, std::make_integer_sequence<int, LSP - NETS * GT::steps()>{});
     put_state<G>(st, S, X, lane);  // g_in: the gradient of z_{l-1} (natural order)
     wsync();
   }
@@ -1176,9 +1215,21 @@ size_t w16_lds(const Shape& s) { return (size_t)kWaves * (kRows * (s.D | 1) + s.
 
 // per layer: the forward stream and biases (all layers first), then the
 // transposed stream of the reverse sweep (after the L forward records)
+// transposed-stream floats per layer (pads included: G16T::lsp)
+// forward A-stream floats per layer (pads included: G16::lsp)
+static int64_t w16_la(const WEntry16* e, int nets) {
+  const int ls = nets * (e->na / 64);
+  return (int64_t)(CNF_W16_FWD_P16 ? (ls + 15) / 16 * 16 : ls) * 64;
+}
+
+static int64_t w16_lt(const WEntry16* e, int nets) {
+  const int ls = nets * (e->nat / 64);
+  return (int64_t)(CNF_W16_BWD_P16 ? (ls + 15) / 16 * 16 : ls) * 64;
+}
+
 int64_t wide16_layer_floats(const Shape& s) {
   const WEntry16* e = w16find(s);
-  return e ? (int64_t)(e->na + e->nb + e->nat) * s.nets : 0;
+  return e ? w16_la(e, s.nets) + (int64_t)s.nets * e->nb + w16_lt(e, s.nets) : 0;
 }
 
 int wide16_prepare(const Shape& s, const float* const* params, void* prepared, hipStream_t st) {
@@ -1186,8 +1237,8 @@ int wide16_prepare(const Shape& s, const float* const* params, void* prepared, h
   if (!e) return CNF_OK;
   float* region = reinterpret_cast<float*>(static_cast<char*>(prepared) + idx_bytes(s)) +
                   s.wide_region;
-  const int64_t LA = (int64_t)s.nets * e->na, LF = LA + (int64_t)s.nets * e->nb;
-  const int64_t LT = (int64_t)s.nets * e->nat;
+  const int64_t LA = w16_la(e, s.nets), LF = LA + (int64_t)s.nets * e->nb;
+  const int64_t LT = w16_lt(e, s.nets);
   int pi = 0;
   for (int l = 0; l < s.L; ++l) {
     WPrep16 a{};
@@ -1306,7 +1357,7 @@ int wide16_train_backward(const Shape& s, const void* prepared, const float* gz,
   const char* base = static_cast<const char*>(prepared);
   const int32_t* inv_q = reinterpret_cast<const int32_t*>(base) + s.L * s.D;
   const float* W = reinterpret_cast<const float*>(base + idx_bytes(s)) + s.wide_region;
-  const int64_t LF = (int64_t)s.nets * (e->na + e->nb);
+  const int64_t LF = w16_la(e, s.nets) + (int64_t)s.nets * e->nb;
   const int64_t rows_per_block = (int64_t)kRows * kWaves;
   const dim3 grid((unsigned)((B + rows_per_block - 1) / rows_per_block)), block(64 * kWaves);
   hipLaunchKernelGGL(e->tbwd[s.nets - 1], grid, block, w16_lds(s), st, W + s.L * LF, inv_q, gz,
