@@ -16,8 +16,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def kernels(obj):
     with tempfile.TemporaryDirectory() as d:
         fat, co = os.path.join(d, "fat.bin"), os.path.join(d, "co.o")
-        r = subprocess.run([BIN + "/llvm-objcopy", "--dump-section=.hip_fatbin=" + fat, obj],
-                           capture_output=True)
+        # an explicit output file: with none, objcopy rewrites the object in
+        # place (a newer mtime makes the next make relink for nothing)
+        r = subprocess.run([BIN + "/llvm-objcopy", "--dump-section=.hip_fatbin=" + fat, obj,
+                            os.path.join(d, "copy.o")], capture_output=True)
         if r.returncode != 0:  # host-only object (no device code)
             return []
         subprocess.run([BIN + "/clang-offload-bundler", "--type=o", "--unbundle",
