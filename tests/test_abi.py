@@ -132,3 +132,32 @@ def test_torch_library_operators_register():
     assert "Tensor[] params" in sch and "int[] desc" in sch
     d = _lib.make_desc(10, 6, [5, 5])
     assert _lib.desc_list(d) == [10, 6, 2, 5, 5, 0, 0, 0, 0, 0, 0, 1, 1, 0, 0]
+
+
+def _vjp_bytes(desc, B):
+    n = ctypes.c_size_t()
+    st = _lib.lib().cnf_vjp_workspace_bytes(ctypes.byref(desc), ctypes.c_int64(B), ctypes.byref(n))
+    return st, n.value
+
+
+def test_wide_training_workspace_plans():
+    """cfg4 at 2^18 rows: the fused sweeps' plan holds the per-row tape (640
+    floats per row and layer) and every layer's conditioner gradients (576), in
+    whole 32-row blocks; OPT_NO_WIDE, strict_nan and the inverse take the
+    layer-at-a-time plan (host-only sizing, no GPU)."""
+    B, L = 1 << 18, 12
+    st, fused = _vjp_bytes(_lib.make_desc(100, L, [100, 100]), B)
+    assert st == 0
+    tape_and_g = L * B * (640 + 576) * 4
+    assert tape_and_g < fused < tape_and_g * 1.05
+    st, layered = _vjp_bytes(_lib.make_desc(100, L, [100, 100], options=_lib.OPT_NO_WIDE), B)
+    assert st == 0 and layered < tape_and_g
+    st, strict = _vjp_bytes(_lib.make_desc(100, L, [100, 100], strict_nan=True), B)
+    assert st == 0 and strict < tape_and_g
+    n = ctypes.c_size_t()
+    assert _lib.lib().cnf_vjp_inverse_workspace_bytes(
+        ctypes.byref(_lib.make_desc(100, L, [100, 100])), ctypes.c_int64(B), ctypes.byref(n)) == 0
+    assert n.value == layered
+    # a ragged batch: the wave-tiled arrays hold whole 32-row blocks
+    st, ragged = _vjp_bytes(_lib.make_desc(100, L, [100, 100]), B + 1)
+    assert st == 0 and ragged > L * (B + 32) * (640 + 576) * 4
