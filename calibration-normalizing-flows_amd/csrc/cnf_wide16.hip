@@ -57,6 +57,13 @@ typedef float v4 __attribute__((ext_vector_type(4)));
 
 constexpr int kRows = 32;   // rows per wave (two row groups of 16)
 constexpr int kWaves = 4;   // waves per block
+// row groups per wave of the inference kernel (k_wide16): 2 -> 32 rows per
+// wave at 2 waves per SIMD; 4 -> 64 rows per wave at 1 wave per SIMD
+#ifndef CNF_W16_RUN_RG
+#define CNF_W16_RUN_RG 2
+#endif
+constexpr int kRunRG = CNF_W16_RUN_RG, kRunRows = 16 * kRunRG;
+static_assert(kRunRG == 2 || kRunRG == 4, "CNF_W16_RUN_RG: 2 or 4");
 
 // the slot of unit u (and, the map being an involution, the unit of slot u)
 __host__ __device__ constexpr int qslot(int u) {
@@ -119,17 +126,18 @@ __device__ __forceinline__ void wsync() {
 // refilled P fragments ahead along the layer's A stream (both nets, every
 // Linear) and on into the next layer's (an).  Both row groups.
 // The B operand is tile TOFF + N / 4 of `in`.
-template <class G, int NETS, int NET, int I, int MO, int N, int TOFF, int P, int TIN>
-__device__ __forceinline__ void kstep(v4 (&acc)[2], float (&ring)[P], const float* __restrict__ a,
-                                      const float* __restrict__ an, const v4 (&in)[TIN][2]) {
+template <class G, int NETS, int NET, int I, int MO, int N, int TOFF, int P, int TIN, int RG>
+__device__ __forceinline__ void kstep(v4 (&acc)[RG], float (&ring)[P], const float* __restrict__ a,
+                                      const float* __restrict__ an, const v4 (&in)[TIN][RG]) {
   constexpr int LS = G::template lsp<NETS>();  // stream steps per layer (pads included)
   constexpr int T = NET * G::steps() + G::sbefore(I) + MO * G::ks(I) + N;
   const float av = ring[T % P];
   if constexpr (T + P < LS) ring[T % P] = a[(T + P) * 64];
   else ring[T % P] = an[(T + P - LS) * 64];
   constexpr int t = TOFF + (N >> 2), q = N & 3;
-  acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, in[t][0][q], acc[0], 0, 0, 0);
-  acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, in[t][1][q], acc[1], 0, 0, 0);
+#pragma unroll
+  for (int g = 0; g < RG; ++g)
+    acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, in[t][g][q], acc[g], 0, 0, 0);
   // keep each refill where it is (left alone, the scheduler sinks the loads
   // next to their use and every MFMA waits for memory)
   __builtin_amdgcn_sched_barrier(0);
@@ -155,15 +163,15 @@ __device__ __forceinline__ void pad_steps(float (&ring)[P], const float* __restr
 // output), or the fused affine update of the state (the s-net's last Linear).
 // pre<MO>() runs before M-tile MO's K-steps (operand prefetch), put<MO>(acc)
 // after them.
-template <bool RELU, int TOUT>
+template <bool RELU, int TOUT, int RG = 2>
 struct EpOut {
-  v4 (&o)[TOUT][2];
+  v4 (&o)[TOUT][RG];
   template <int MO>
   __device__ __forceinline__ void pre() {}
   template <int MO>
-  __device__ __forceinline__ void put(v4 (&acc)[2]) {
+  __device__ __forceinline__ void put(v4 (&acc)[RG]) {
 #pragma unroll
-    for (int g = 0; g < 2; ++g) {
+    for (int g = 0; g < RG; ++g) {
       if constexpr (RELU) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) acc[g][q] = fmaxf(acc[g][q], 0.f);
@@ -173,17 +181,17 @@ struct EpOut {
   }
 };
 
-template <bool INV, int XT, int CT, int TT>
+template <bool INV, int XT, int CT, int TT, int RG = 2>
 struct EpAffine {
-  v4 (&X)[XT][2];
-  const v4 (&T)[TT][2];
-  float (&ld)[2];
+  v4 (&X)[XT][RG];
+  const v4 (&T)[TT][RG];
+  float (&ld)[RG];
   template <int MO>
   __device__ __forceinline__ void pre() {}
   template <int MO>
-  __device__ __forceinline__ void put(v4 (&s)[2]) {
+  __device__ __forceinline__ void put(v4 (&s)[RG]) {
 #pragma unroll
-    for (int g = 0; g < 2; ++g)
+    for (int g = 0; g < RG; ++g)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         // padding slots get s = t = 0 (zero weights and bias): x stays x
@@ -210,26 +218,29 @@ __device__ __forceinline__ v4 bias_load(const float* __restrict__ bias, int lane
   }
 }
 
-template <class G, int NETS, int NET, int I, int MO, int TOFF, int P, int TIN, class EP, int... N>
+template <class G, int NETS, int NET, int I, int MO, int TOFF, int P, int TIN, int RG, class EP,
+          int... N>
 __device__ __forceinline__ void mtile(float (&ring)[P], const float* __restrict__ a,
                                       const float* __restrict__ an,
-                                      const float* __restrict__ bias, const v4 (&in)[TIN][2],
+                                      const float* __restrict__ bias, const v4 (&in)[TIN][RG],
                                       EP& ep, int lane, std::integer_sequence<int, N...>) {
-  v4 acc[2] = {v4{0.f, 0.f, 0.f, 0.f}, v4{0.f, 0.f, 0.f, 0.f}};
+  v4 acc[RG];
+#pragma unroll
+  for (int g = 0; g < RG; ++g) acc[g] = v4{0.f, 0.f, 0.f, 0.f};
   ep.template pre<MO>();
   const v4 b = bias_load<G, I, MO>(bias, lane);
   (kstep<G, NETS, NET, I, MO, N, TOFF, P>(acc, ring, a, an, in), ...);
   if constexpr (G::kBias) {
-    acc[0] += b;
-    acc[1] += b;
+#pragma unroll
+    for (int g = 0; g < RG; ++g) acc[g] += b;
   }
   ep.template put<MO>(acc);
 }
 
-template <class G, int NETS, int NET, int I, int TOFF, int P, int TIN, class EP, int... M>
+template <class G, int NETS, int NET, int I, int TOFF, int P, int TIN, int RG, class EP, int... M>
 __device__ __forceinline__ void lin(float (&ring)[P], const float* __restrict__ a,
                                     const float* __restrict__ an, const float* __restrict__ bias,
-                                    const v4 (&in)[TIN][2], EP& ep, int lane,
+                                    const v4 (&in)[TIN][RG], EP& ep, int lane,
                                     std::integer_sequence<int, M...>) {
   (mtile<G, NETS, NET, I, M, TOFF>(ring, a, an, bias, in, ep, lane,
                              std::make_integer_sequence<int, G::ks(I)>{}),
@@ -238,23 +249,23 @@ __device__ __forceinline__ void lin(float (&ring)[P], const float* __restrict__ 
 
 // One conditioner MLP (stream position NET of the layer) on the state's
 // conditioning tiles; its last Linear's tiles go to ep.
-template <class G, int NETS, int NET, int P, class EP>
+template <class G, int NETS, int NET, int P, class EP, int RG>
 __device__ __forceinline__ void net(float (&ring)[P], const float* __restrict__ a,
                                     const float* __restrict__ an, const float* __restrict__ bias,
-                                    const v4 (&X)[G::XT][2], EP& ep, int lane) {
+                                    const v4 (&X)[G::XT][RG], EP& ep, int lane) {
   using MS0 = std::make_integer_sequence<int, G::mt(0)>;
   if constexpr (G::NL == 1) {
     lin<G, NETS, NET, 0, 0>(ring, a, an, bias, X, ep, lane, MS0{});
   } else if constexpr (G::NL == 2) {
-    v4 h1[G::T1][2];
-    EpOut<true, G::T1> e1{h1};
+    v4 h1[G::T1][RG];
+    EpOut<true, G::T1, RG> e1{h1};
     lin<G, NETS, NET, 0, 0>(ring, a, an, bias, X, e1, lane, MS0{});
     lin<G, NETS, NET, 1, 0>(ring, a, an, bias, h1, ep, lane,
                          std::make_integer_sequence<int, G::mt(1)>{});
   } else {
-    v4 h1[G::T1][2], h2[G::T2][2];
-    EpOut<true, G::T1> e1{h1};
-    EpOut<true, G::T2> e2{h2};
+    v4 h1[G::T1][RG], h2[G::T2][RG];
+    EpOut<true, G::T1, RG> e1{h1};
+    EpOut<true, G::T2, RG> e2{h2};
     lin<G, NETS, NET, 0, 0>(ring, a, an, bias, X, e1, lane, MS0{});
     lin<G, NETS, NET, 1, 0>(ring, a, an, bias, h1, e2, lane,
                          std::make_integer_sequence<int, G::mt(1)>{});
@@ -264,12 +275,12 @@ __device__ __forceinline__ void net(float (&ring)[P], const float* __restrict__ 
 }
 
 // state slots -> LDS rows [row][feature]
-template <class G>
-__device__ __forceinline__ void put_state(float* st, int S, const v4 (&X)[G::XT][2], int lane) {
+template <class G, int RG>
+__device__ __forceinline__ void put_state(float* st, int S, const v4 (&X)[G::XT][RG], int lane) {
 #pragma unroll
   for (int t = 0; t < G::XT; ++t)
 #pragma unroll
-    for (int g = 0; g < 2; ++g)
+    for (int g = 0; g < RG; ++g)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int f = feat_of<G>(16 * t + 4 * (lane >> 4) + q);
@@ -279,13 +290,13 @@ __device__ __forceinline__ void put_state(float* st, int S, const v4 (&X)[G::XT]
 
 // state slots <- LDS rows through a gather table (slot of feature f takes
 // logical q[f]; q == nullptr: identity)
-template <class G>
-__device__ __forceinline__ void get_state(const float* st, int S, const int* qs, v4 (&X)[G::XT][2],
+template <class G, int RG>
+__device__ __forceinline__ void get_state(const float* st, int S, const int* qs, v4 (&X)[G::XT][RG],
                                           int lane) {
 #pragma unroll
   for (int t = 0; t < G::XT; ++t)
 #pragma unroll
-    for (int g = 0; g < 2; ++g)
+    for (int g = 0; g < RG; ++g)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int f = feat_of<G>(16 * t + 4 * (lane >> 4) + q);
@@ -293,9 +304,9 @@ __device__ __forceinline__ void get_state(const float* st, int S, const int* qs,
       }
 }
 
-template <class G>
+template <class G, int RG>
 __device__ __forceinline__ void relayout(float* st, int* qs, int S, const int32_t* __restrict__ q,
-                                         v4 (&X)[G::XT][2], int lane) {
+                                         v4 (&X)[G::XT][RG], int lane) {
   for (int j = lane; j < G::DT + G::DC; j += 64) qs[j] = q[j];
   put_state<G>(st, S, X, lane);
   wsync();
@@ -353,7 +364,7 @@ __device__ __forceinline__ void row_predict16(float* st, int S, int lane,
 
 // MODE 0 forward, 1 inverse, 2 predict (centre + forward + calibrated probs)
 template <int D, int H1, int H2, int MODE, int NETS>
-__global__ __launch_bounds__(64 * kWaves, 2) void k_wide16(
+__global__ __launch_bounds__(64 * kWaves, kRunRG == 2 ? 2 : 1) void k_wide16(
     const float* __restrict__ W, const int32_t* __restrict__ qtab,
     const float* __restrict__ in, float* __restrict__ out, float* __restrict__ ld_out,
     int64_t B, int L, const float* __restrict__ lpri) {
@@ -366,24 +377,24 @@ __global__ __launch_bounds__(64 * kWaves, 2) void k_wide16(
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // SGPR: row0, descriptors
-  const int64_t row0 = ((int64_t)blockIdx.x * kWaves + wave) * kRows;
+  const int64_t row0 = ((int64_t)blockIdx.x * kWaves + wave) * kRunRows;
   if (row0 >= B) return;  // waves synchronise only with themselves
-  const int nrows = (int)((B - row0) < kRows ? (B - row0) : kRows);
-  float* st = smem + wave * (kRows * S + D);
-  int* qs = reinterpret_cast<int*>(st + kRows * S);
+  const int nrows = (int)((B - row0) < kRunRows ? (B - row0) : kRunRows);
+  float* st = smem + wave * (kRunRows * S + D);
+  int* qs = reinterpret_cast<int*>(st + kRunRows * S);
 
   // rows -> LDS (coalesced) -> slots
   const float* src = in + row0 * D;
-  for (int i = lane; i < kRows * D; i += 64) {
+  for (int i = lane; i < kRunRows * D; i += 64) {
     const int r = i / D, f = i - r * D;
     st[r * S + f] = r < nrows ? src[i] : 0.f;
   }
   wsync();
   if constexpr (MODE == 2) {  // x - mean(x) per row (calibrators.py:42)
-    row_centre16<D>(st, S, lane);
+    for (int rb = 0; rb < kRunRows; rb += 32) row_centre16<D>(st + rb * S, S, lane);
     wsync();
   }
-  v4 X[XT][2];
+  v4 X[XT][kRunRG];
   get_state<G>(st, S, nullptr, X, lane);
   wsync();
 
@@ -395,7 +406,7 @@ __global__ __launch_bounds__(64 * kWaves, 2) void k_wide16(
 #pragma unroll
     for (int j = 0; j < P; ++j) ring[j] = a0[j * 64];
   }
-  float ld[2] = {0.f, 0.f};
+  float ld[kRunRG] = {};
   for (int stp = 0; stp < L; ++stp) {
     const int l = INV ? L - 1 - stp : stp;
     const int ln = stp + 1 < L ? (INV ? l - 1 : l + 1) : l;  // last layer: harmless re-read
@@ -404,18 +415,18 @@ __global__ __launch_bounds__(64 * kWaves, 2) void k_wide16(
     const float* __restrict__ wl = W + (int64_t)l * LF + lane;
     const float* __restrict__ wn = W + (int64_t)ln * LF + lane;
     const float* __restrict__ bl = W + (int64_t)l * LF + LA;  // the layer's bias blocks
-    v4 Tv[TT][2];
-    EpOut<false, TT> et{Tv};
+    v4 Tv[TT][kRunRG];
+    EpOut<false, TT, kRunRG> et{Tv};
     if constexpr (NETS == 2) {  // stream order (prepare): t-net, then s-net
       net<G, 2, 0>(ring, wl, wn, bl, X, et, lane);
-      EpAffine<INV, XT, CT, TT> ea{X, Tv, ld};
+      EpAffine<INV, XT, CT, TT, kRunRG> ea{X, Tv, ld};
       net<G, 2, 1>(ring, wl, wn, bl + G::NB, X, ea, lane);
     } else {
       net<G, 1, 0>(ring, wl, wn, bl, X, et, lane);
 #pragma unroll
       for (int t = 0; t < TT; ++t)
 #pragma unroll
-        for (int g = 0; g < 2; ++g) X[CT + t][g] = INV ? X[CT + t][g] - Tv[t][g] : X[CT + t][g] + Tv[t][g];
+        for (int g = 0; g < kRunRG; ++g) X[CT + t][g] = INV ? X[CT + t][g] - Tv[t][g] : X[CT + t][g] + Tv[t][g];
     }
     pad_steps<G, NETS, P>(ring, wl, wn, std::make_integer_sequence<int, LSP - NETS * G::steps()>{});
     if constexpr (!INV) relayout<G>(st, qs, S, q, X, lane);  // perm then flip
@@ -425,7 +436,7 @@ __global__ __launch_bounds__(64 * kWaves, 2) void k_wide16(
   put_state<G>(st, S, X, lane);
   wsync();
   if constexpr (MODE == 2) {
-    row_predict16<D>(st, S, lane, lpri);
+    for (int rb = 0; rb < kRunRows; rb += 32) row_predict16<D>(st + rb * S, S, lane, lpri);
     wsync();
   }
   if (out) {
@@ -437,13 +448,13 @@ __global__ __launch_bounds__(64 * kWaves, 2) void k_wide16(
   }
   // a row's log-det terms are spread over the four lane groups (l >> 4)
 #pragma unroll
-  for (int g = 0; g < 2; ++g) {
+  for (int g = 0; g < kRunRG; ++g) {
     ld[g] += __shfl_xor(ld[g], 16);
     ld[g] += __shfl_xor(ld[g], 32);
   }
   if (ld_out && lane < 16) {
 #pragma unroll
-    for (int g = 0; g < 2; ++g)
+    for (int g = 0; g < kRunRG; ++g)
       if (16 * g + lane < nrows) ld_out[row0 + 16 * g + lane] = ld[g];
   }
 }
@@ -1209,7 +1220,9 @@ const WEntry16* w16find(const Shape& s) {
   return nullptr;
 }
 
-size_t w16_lds(const Shape& s) { return (size_t)kWaves * (kRows * (s.D | 1) + s.D) * 4; }
+size_t w16_lds(const Shape& s, int rows = kRows) {
+  return (size_t)kWaves * (rows * (s.D | 1) + s.D) * 4;
+}
 
 }  // namespace
 
@@ -1298,10 +1311,10 @@ int wide16_run(const Shape& s, const void* prepared, const float* in, float* out
   const int32_t* fwd_q = reinterpret_cast<const int32_t*>(base);
   const int32_t* inv_q = fwd_q + s.L * s.D;
   const float* W = reinterpret_cast<const float*>(base + idx_bytes(s)) + s.wide_region;
-  const int64_t rows_per_block = (int64_t)kRows * kWaves;
+  const int64_t rows_per_block = (int64_t)kRunRows * kWaves;
   const dim3 grid((unsigned)((B + rows_per_block - 1) / rows_per_block)), block(64 * kWaves);
   WFn fn = e->fn[s.nets - 1][log_priors ? 2 : (inverse ? 1 : 0)];
-  hipLaunchKernelGGL(fn, grid, block, w16_lds(s), st, W, inverse ? inv_q : fwd_q, in, out, ld, B,
+  hipLaunchKernelGGL(fn, grid, block, w16_lds(s, kRunRows), st, W, inverse ? inv_q : fwd_q, in, out, ld, B,
                      s.L, log_priors);
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) {
