@@ -55,6 +55,20 @@ typedef float v4 __attribute__((ext_vector_type(4)));
 #define CNF_W16_BWD_P16 1  // pad the reverse stream per layer to 16-step multiples
 #endif
 
+// A-stream layout: 0 fragment-major (step T, lane l at 64 T + l: one dword
+// load per lane and K-step); 1 four steps interleaved per lane (steps 4j..4j+3
+// of lane l at 256 j + 4 l: one 16-B load per lane every four K-steps)
+#ifndef CNF_W16_PACK4
+#define CNF_W16_PACK4 1
+#endif
+#ifndef CNF_W16_REFILL  // packed layout: steps per refill load (4: 16 B, 2: 8 B per lane)
+#define CNF_W16_REFILL 4
+#endif
+constexpr bool kPack4 = CNF_W16_PACK4 != 0;
+constexpr int kLaneStride = kPack4 ? 4 : 1;  // a lane's first float of a step group
+// float offset (lane 0) of stream step T
+__host__ __device__ constexpr int afrag(int T) { return kPack4 ? (T >> 2) * 256 + (T & 3) : T * 64; }
+
 constexpr int kRows = 32;   // rows per wave (two row groups of 16)
 constexpr int kWaves = 4;   // waves per block
 // row groups per wave of the inference kernel (k_wide16): 2 -> 32 rows per
@@ -70,6 +84,11 @@ __host__ __device__ constexpr int qslot(int u) {
   return 16 * (u >> 4) + 4 * (u & 3) + ((u & 15) >> 2);
 }
 __host__ __device__ constexpr int cdiv(int a, int b) { return (a + b - 1) / b; }
+// a layer's stream steps with its pads (16-step multiples when p16, 4-step
+// multiples for the packed layout)
+__host__ __device__ constexpr int pad_ls(int ls, bool p16) {
+  return p16 ? cdiv(ls, 16) * 16 : (kPack4 ? cdiv(ls, 4) * 4 : ls);
+}
 
 // Compile-time geometry of one conditioner MLP (H = 0: absent hidden layer).
 template <int D, int H1, int H2>
@@ -93,7 +112,7 @@ struct G16 {
   // A-stream steps per layer: padded to a multiple of 16 (a few fragments no
   // MFMA uses) so the ring can be 16 deep (G16T below)
   template <int NETS>
-  static constexpr int lsp() { return CNF_W16_FWD_P16 ? cdiv(NETS * steps(), 16) * 16 : NETS * steps(); }
+  static constexpr int lsp() { return pad_ls(NETS * steps(), CNF_W16_FWD_P16); }
   static constexpr int T1 = H1 > 0 ? cdiv(H1, 16) : 1, T2 = H2 > 0 ? cdiv(H2, 16) : 1;
 };
 
@@ -108,13 +127,49 @@ __device__ __forceinline__ int feat_of(int s) {
   return u < G::DT ? u : -1;
 }
 
+// knock-out A/B builds only (results wrong): 1 no A-ring refills, 2 no
+// per-layer relayout in k_wide16, 4 no exp in the affine epilogue
+#ifndef CNF_W16_KO
+#define CNF_W16_KO 0
+#endif
+
 // A-operand ring depth: the deepest divisor of the layer's step count in
 // [6, pmax] (the ring runs on across layers)
 __host__ __device__ constexpr int ring16(int ls, int pmax) {
   for (int p = pmax; p >= 6; --p)
-    if (ls % p == 0) return p;
-  return 1;
+    if (ls % p == 0 && (!kPack4 || p % 4 == 0)) return p;
+  return kPack4 ? 4 : 1;
 }
+
+// the ring's refill at stream step T (fragment T + P into the slot step T
+// just used); packed: every fourth step, the four slots steps T-3..T used
+// (a 16-B load per lane)
+template <class G, int NETS, int P, int T>
+__device__ __forceinline__ void refill(float (&ring)[P], const float* __restrict__ a,
+                                       const float* __restrict__ an) {
+  constexpr int LS = G::template lsp<NETS>();  // stream steps per layer (pads included)
+  if constexpr (CNF_W16_KO & 1) {
+  } else if constexpr (!kPack4) {
+    if constexpr (T + P < LS) ring[T % P] = a[afrag(T + P)];
+    else ring[T % P] = an[afrag(T + P - LS)];
+  } else if constexpr (CNF_W16_REFILL == 4 && (T & 3) == 3) {
+    static_assert(P % 4 == 0 && LS % 4 == 0, "packed A stream: ring and layer in 4-step groups");
+    constexpr int S0 = T - 3 + P;  // first step refilled (a multiple of 4)
+    const v4 v = *reinterpret_cast<const v4*>(S0 < LS ? a + afrag(S0) : an + afrag(S0 - LS));
+    ring[(T - 3) % P] = v[0];
+    ring[(T - 2) % P] = v[1];
+    ring[(T - 1) % P] = v[2];
+    ring[T % P] = v[3];
+  } else if constexpr (CNF_W16_REFILL == 2 && (T & 1) == 1) {
+    static_assert(P % 4 == 0 && LS % 4 == 0, "packed A stream: ring and layer in 4-step groups");
+    constexpr int S0 = T - 1 + P;  // first step refilled (even)
+    typedef float v2 __attribute__((ext_vector_type(2)));
+    const v2 v = *reinterpret_cast<const v2*>(S0 < LS ? a + afrag(S0) : an + afrag(S0 - LS));
+    ring[(T - 1) % P] = v[0];
+    ring[T % P] = v[1];
+  }
+}
+
 
 __device__ __forceinline__ void wsync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -129,11 +184,9 @@ __device__ __forceinline__ void wsync() {
 template <class G, int NETS, int NET, int I, int MO, int N, int TOFF, int P, int TIN, int RG>
 __device__ __forceinline__ void kstep(v4 (&acc)[RG], float (&ring)[P], const float* __restrict__ a,
                                       const float* __restrict__ an, const v4 (&in)[TIN][RG]) {
-  constexpr int LS = G::template lsp<NETS>();  // stream steps per layer (pads included)
   constexpr int T = NET * G::steps() + G::sbefore(I) + MO * G::ks(I) + N;
   const float av = ring[T % P];
-  if constexpr (T + P < LS) ring[T % P] = a[(T + P) * 64];
-  else ring[T % P] = an[(T + P - LS) * 64];
+  refill<G, NETS, P, T>(ring, a, an);
   constexpr int t = TOFF + (N >> 2), q = N & 3;
 #pragma unroll
   for (int g = 0; g < RG; ++g)
@@ -147,9 +200,7 @@ __device__ __forceinline__ void kstep(v4 (&acc)[RG], float (&ring)[P], const flo
 template <class G, int NETS, int P, int T>
 __device__ __forceinline__ void pad_step(float (&ring)[P], const float* __restrict__ a,
                                          const float* __restrict__ an) {
-  constexpr int LS = G::template lsp<NETS>();
-  if constexpr (T + P < LS) ring[T % P] = a[(T + P) * 64];
-  else ring[T % P] = an[(T + P - LS) * 64];
+  refill<G, NETS, P, T>(ring, a, an);
   __builtin_amdgcn_sched_barrier(0);
 }
 template <class G, int NETS, int P, int... K>
@@ -196,7 +247,7 @@ struct EpAffine {
       for (int q = 0; q < 4; ++q) {
         // padding slots get s = t = 0 (zero weights and bias): x stays x
         const float sv = s[g][q];
-        const float e = __builtin_amdgcn_exp2f((INV ? -sv : sv) * 1.4426950408889634f);
+        const float e = (CNF_W16_KO & 4) ? sv : __builtin_amdgcn_exp2f((INV ? -sv : sv) * 1.4426950408889634f);
         const float x = X[CT + MO][g][q];
         X[CT + MO][g][q] = INV ? (x - T[MO][g][q]) * e : fmaf(x, e, T[MO][g][q]);
         ld[g] += INV ? -sv : sv;
@@ -402,18 +453,18 @@ __global__ __launch_bounds__(64 * kWaves, kRunRG == 2 ? 2 : 1) void k_wide16(
   constexpr int P = ring16(LSP, CNF_W16_PMAX);
   float ring[P];
   {
-    const float* a0 = W + (int64_t)(INV ? L - 1 : 0) * LF + lane;
+    const float* a0 = W + (int64_t)(INV ? L - 1 : 0) * LF + kLaneStride * lane;
 #pragma unroll
-    for (int j = 0; j < P; ++j) ring[j] = a0[j * 64];
+    for (int j = 0; j < P; ++j) ring[j] = a0[afrag(j)];
   }
   float ld[kRunRG] = {};
   for (int stp = 0; stp < L; ++stp) {
     const int l = INV ? L - 1 - stp : stp;
     const int ln = stp + 1 < L ? (INV ? l - 1 : l + 1) : l;  // last layer: harmless re-read
     const int32_t* __restrict__ q = qtab + l * D;
-    if constexpr (INV) relayout<G>(st, qs, S, q, X, lane);  // flip / rev_perm first
-    const float* __restrict__ wl = W + (int64_t)l * LF + lane;
-    const float* __restrict__ wn = W + (int64_t)ln * LF + lane;
+    if constexpr (INV && !(CNF_W16_KO & 2)) relayout<G>(st, qs, S, q, X, lane);  // flip / rev_perm first
+    const float* __restrict__ wl = W + (int64_t)l * LF + kLaneStride * lane;
+    const float* __restrict__ wn = W + (int64_t)ln * LF + kLaneStride * lane;
     const float* __restrict__ bl = W + (int64_t)l * LF + LA;  // the layer's bias blocks
     v4 Tv[TT][kRunRG];
     EpOut<false, TT, kRunRG> et{Tv};
@@ -429,7 +480,7 @@ __global__ __launch_bounds__(64 * kWaves, kRunRG == 2 ? 2 : 1) void k_wide16(
         for (int g = 0; g < kRunRG; ++g) X[CT + t][g] = INV ? X[CT + t][g] - Tv[t][g] : X[CT + t][g] + Tv[t][g];
     }
     pad_steps<G, NETS, P>(ring, wl, wn, std::make_integer_sequence<int, LSP - NETS * G::steps()>{});
-    if constexpr (!INV) relayout<G>(st, qs, S, q, X, lane);  // perm then flip
+    if constexpr (!INV && !(CNF_W16_KO & 2)) relayout<G>(st, qs, S, q, X, lane);  // perm then flip
   }
 
   // slots -> LDS rows -> coalesced stores
@@ -488,7 +539,7 @@ struct G16T {
   // steps, can then be 16 deep instead of 12, and every tape / G access gets 16
   // K-steps to complete before a ring wait covers it (vmcnt counts in order).
   template <int NETS>
-  static constexpr int lsp() { return CNF_W16_BWD_P16 ? cdiv(NETS * steps(), 16) * 16 : NETS * steps(); }
+  static constexpr int lsp() { return pad_ls(NETS * steps(), CNF_W16_BWD_P16); }
 };
 
 
@@ -809,12 +860,12 @@ __global__ __launch_bounds__(64 * kWaves, 2) void k_wtrain16_fwd(
   constexpr int P = ring16(LSP, CNF_W16_PMAX);
   float ring[P];
 #pragma unroll
-  for (int j = 0; j < P; ++j) ring[j] = W[lane + j * 64];
+  for (int j = 0; j < P; ++j) ring[j] = W[kLaneStride * lane + afrag(j)];
   float ld[2] = {0.f, 0.f};
   for (int l = 0; l < L; ++l) {
     const int ln = l + 1 < L ? l + 1 : l;
-    const float* __restrict__ wl = W + (int64_t)l * LF + lane;
-    const float* __restrict__ wn = W + (int64_t)ln * LF + lane;
+    const float* __restrict__ wl = W + (int64_t)l * LF + kLaneStride * lane;
+    const float* __restrict__ wn = W + (int64_t)ln * LF + kLaneStride * lane;
     const float* __restrict__ bl = W + (int64_t)l * LF + LA;
     const Rows16 tp(tape + ((int64_t)l * nwb * kRows + row0) * TP::RW, TP::RW, lane);
 #pragma unroll
@@ -997,9 +1048,9 @@ __global__ __launch_bounds__(64 * kWaves, 2) void k_wtrain16_bwd(
   constexpr int P = ring16(LSP, CNF_W16_PMAX);
   float ring[P];
   {
-    const float* a0 = WT + (int64_t)(L - 1) * LT + lane;
+    const float* a0 = WT + (int64_t)(L - 1) * LT + kLaneStride * lane;
 #pragma unroll
-    for (int j = 0; j < P; ++j) ring[j] = a0[j * 64];
+    for (int j = 0; j < P; ++j) ring[j] = a0[afrag(j)];
   }
   float gl[2];
 #pragma unroll
@@ -1043,8 +1094,8 @@ __global__ __launch_bounds__(64 * kWaves, 2) void k_wtrain16_bwd(
     wsync();
     get_state<G>(st, S, qs, X, lane);
     wsync();
-    const float* __restrict__ wa = WT + (int64_t)l * LT + lane;
-    const float* __restrict__ wn = WT + (int64_t)(l > 0 ? l - 1 : l) * LT + lane;
+    const float* __restrict__ wa = WT + (int64_t)l * LT + kLaneStride * lane;
+    const float* __restrict__ wn = WT + (int64_t)(l > 0 ? l - 1 : l) * LT + kLaneStride * lane;
     if constexpr (NETS == 2) {
       v4 Gs[TT][2];
 #pragma unroll
@@ -1109,6 +1160,7 @@ using TBwdFn = void (*)(const float*, const int32_t*, const float*, const float*
 struct WSeg16 {
   const float* W;
   const float* b;
+  int64_t abase;          // float offset of the layer's stream (step 0)
   int64_t adst, bdst;     // float offsets of its A fragments and bias block (-1: none)
   int nm, nk;             // M-tiles, K-steps
   int first;              // the Linear reads the conditioning half (weight columns DT..D-1)
@@ -1136,7 +1188,8 @@ __global__ void k_prepare_wide16(WPrep16 a, float* __restrict__ wreg) {
     float v = 0.f;
     if (o < g.nout && u < g.nin)
       v = g.trans ? g.W[(int64_t)u * g.nin_full + c0 + o] : g.W[(int64_t)o * g.nin_full + c0 + u];
-    wreg[g.adst + e] = v;
+    const int64_t x = g.adst - g.abase + e;  // fragment-major offset in the stream
+    wreg[g.abase + afrag((int)(x >> 6)) + kLaneStride * (x & 63)] = v;
   }
   if (g.bdst < 0 || blockIdx.y != 0) return;
   for (int s = threadIdx.x; s < 16 * g.nm; s += blockDim.x) {
@@ -1232,12 +1285,12 @@ size_t w16_lds(const Shape& s, int rows = kRows) {
 // forward A-stream floats per layer (pads included: G16::lsp)
 static int64_t w16_la(const WEntry16* e, int nets) {
   const int ls = nets * (e->na / 64);
-  return (int64_t)(CNF_W16_FWD_P16 ? (ls + 15) / 16 * 16 : ls) * 64;
+  return (int64_t)pad_ls(ls, CNF_W16_FWD_P16) * 64;
 }
 
 static int64_t w16_lt(const WEntry16* e, int nets) {
   const int ls = nets * (e->nat / 64);
-  return (int64_t)(CNF_W16_BWD_P16 ? (ls + 15) / 16 * 16 : ls) * 64;
+  return (int64_t)pad_ls(ls, CNF_W16_BWD_P16) * 64;
 }
 
 int64_t wide16_layer_floats(const Shape& s) {
@@ -1272,7 +1325,8 @@ int wide16_prepare(const Shape& s, const float* const* params, void* prepared, h
         g.DT = s.DT;
         g.nm = e->mt[i];
         g.nk = e->ks[i];
-        g.adst = (int64_t)l * LF + (int64_t)pos * e->na + e->abefore[i];
+        g.abase = (int64_t)l * LF;
+        g.adst = g.abase + (int64_t)pos * e->na + e->abefore[i];
         g.bdst = (int64_t)l * LF + LA + (int64_t)pos * e->nb + e->bbefore[i];
       }
     }
@@ -1289,7 +1343,8 @@ int wide16_prepare(const Shape& s, const float* const* params, void* prepared, h
         g.nout = f.nin;
         g.nm = e->mtT[r];
         g.nk = e->ksT[r];
-        g.adst = (int64_t)s.L * LF + (int64_t)l * LT + (int64_t)net * e->nat + e->abeforeT[r];
+        g.abase = (int64_t)s.L * LF + (int64_t)l * LT;
+        g.adst = g.abase + (int64_t)net * e->nat + e->abeforeT[r];
         g.bdst = -1;
       }
     hipLaunchKernelGGL(k_prepare_wide16, dim3(a.nseg, 8), dim3(256), 0, st, a, region);
