@@ -89,6 +89,20 @@ __host__ __device__ constexpr int cdiv(int a, int b) { return (a + b - 1) / b; }
 __host__ __device__ constexpr int pad_ls(int ls, bool p16) {
   return p16 ? cdiv(ls, 16) * 16 : (kPack4 ? cdiv(ls, 4) * 4 : ls);
 }
+// k_wide16's A stream through LDS (A/B): the block's four waves copy the stream
+// by LDS-DMA in chunks of kAC steps (one 1-KiB piece per wave) into two stages,
+// and refill their rings from LDS; forward streams padded to 2 kAC steps
+#ifndef CNF_W16_LDSA
+#define CNF_W16_LDSA 1
+#endif
+constexpr int kAC = 16;
+#ifndef CNF_W16_LDSA_PMAX  // k_wide16's ring depth with the LDS stream (LDS latency is short)
+#define CNF_W16_LDSA_PMAX 8
+#endif
+__host__ __device__ constexpr int pad_fwd(int ls) {
+  return CNF_W16_LDSA ? cdiv(ls, 2 * kAC) * 2 * kAC : pad_ls(ls, CNF_W16_FWD_P16);
+}
+extern __shared__ __attribute__((aligned(16))) float w16_dyn[];
 
 // Compile-time geometry of one conditioner MLP (H = 0: absent hidden layer).
 template <int D, int H1, int H2>
@@ -112,8 +126,16 @@ struct G16 {
   // A-stream steps per layer: padded to a multiple of 16 (a few fragments no
   // MFMA uses) so the ring can be 16 deep (G16T below)
   template <int NETS>
-  static constexpr int lsp() { return pad_ls(NETS * steps(), CNF_W16_FWD_P16); }
+  static constexpr int lsp() { return pad_fwd(NETS * steps()); }
+  static constexpr bool kLdsA = false;
   static constexpr int T1 = H1 > 0 ? cdiv(H1, 16) : 1, T2 = H2 > 0 ? cdiv(H2, 16) : 1;
+};
+// k_wide16's geometry when its A stream comes through LDS
+template <int D, int H1, int H2>
+struct G16L : G16<D, H1, H2> {
+  static constexpr bool kLdsA = CNF_W16_LDSA != 0;
+  // floats of the waves' state areas (the A stages follow)
+  static constexpr int kStateFloats = cdiv(kWaves * (kRunRows * (D | 1) + D), 64) * 64;
 };
 
 // feature of state slot s (-1: padding)
@@ -149,6 +171,29 @@ __device__ __forceinline__ void refill(float (&ring)[P], const float* __restrict
                                        const float* __restrict__ an) {
   constexpr int LS = G::template lsp<NETS>();  // stream steps per layer (pads included)
   if constexpr (CNF_W16_KO & 1) {
+  } else if constexpr (G::kLdsA) {
+    static_assert(kPack4 && P % 4 == 0 && P <= kAC && LS % (2 * kAC) == 0, "LDS A stream");
+    if constexpr ((T & 3) == 3) {
+      constexpr int S0 = T - 3 + P;  // first step refilled
+      const int lane = threadIdx.x & 63;
+      float* stage = w16_dyn + G::kStateFloats;
+      if constexpr (S0 % kAC == 0) {
+        // chunk S0 / kAC starts: everyone's pieces of it have landed and everyone
+        // is done with the chunk before it, whose stage the next chunk takes
+        const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        constexpr int S1 = S0 + kAC;  // the next chunk (a = W + layer + 4 lane)
+        const float* src = (S1 < LS ? a + afrag(S1) : an + afrag(S1 - LS)) + 256 * w;
+        __builtin_amdgcn_global_load_lds(const_cast<float*>(src),
+                                         stage + afrag(S1 % (2 * kAC)) + 256 * w, 16, 0, 0);
+      }
+      const v4 v = *reinterpret_cast<const v4*>(stage + afrag(S0 % (2 * kAC)) + 4 * lane);
+      ring[(T - 3) % P] = v[0];
+      ring[(T - 2) % P] = v[1];
+      ring[(T - 1) % P] = v[2];
+      ring[T % P] = v[3];
+    }
   } else if constexpr (!kPack4) {
     if constexpr (T + P < LS) ring[T % P] = a[afrag(T + P)];
     else ring[T % P] = an[afrag(T + P - LS)];
@@ -419,7 +464,7 @@ __global__ __launch_bounds__(64 * kWaves, kRunRG == 2 ? 2 : 1) void k_wide16(
     const float* __restrict__ W, const int32_t* __restrict__ qtab,
     const float* __restrict__ in, float* __restrict__ out, float* __restrict__ ld_out,
     int64_t B, int L, const float* __restrict__ lpri) {
-  using G = G16<D, H1, H2>;
+  using G = G16L<D, H1, H2>;
   constexpr bool INV = MODE == 1;
   constexpr int XT = G::XT, CT = G::CT, TT = G::TT;
   constexpr int S = D | 1;  // odd LDS row stride
@@ -429,7 +474,9 @@ __global__ __launch_bounds__(64 * kWaves, kRunRG == 2 ? 2 : 1) void k_wide16(
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // SGPR: row0, descriptors
   const int64_t row0 = ((int64_t)blockIdx.x * kWaves + wave) * kRunRows;
-  if (row0 >= B) return;  // waves synchronise only with themselves
+  // waves synchronise only with themselves (LDS A stream: the whole block
+  // takes part in every chunk; a wave past the batch computes zero rows)
+  if (!G::kLdsA && row0 >= B) return;
   const int nrows = (int)((B - row0) < kRunRows ? (B - row0) : kRunRows);
   float* st = smem + wave * (kRunRows * S + D);
   int* qs = reinterpret_cast<int*>(st + kRunRows * S);
@@ -450,12 +497,24 @@ __global__ __launch_bounds__(64 * kWaves, kRunRG == 2 ? 2 : 1) void k_wide16(
   wsync();
 
   // the A stream: one ring for the whole launch, P fragments ahead of the MFMAs
-  constexpr int P = ring16(LSP, CNF_W16_PMAX);
+  constexpr int P = ring16(LSP, G::kLdsA ? CNF_W16_LDSA_PMAX : CNF_W16_PMAX);
   float ring[P];
   {
     const float* a0 = W + (int64_t)(INV ? L - 1 : 0) * LF + kLaneStride * lane;
+    if constexpr (G::kLdsA) {  // chunks 0 and 1 of the first layer, then the ring from LDS
+      float* stage = w16_dyn + G::kStateFloats;
 #pragma unroll
-    for (int j = 0; j < P; ++j) ring[j] = a0[afrag(j)];
+      for (int c = 0; c < 2; ++c)
+        __builtin_amdgcn_global_load_lds(const_cast<float*>(a0 + afrag(c * kAC) + 256 * wave),
+                                         stage + afrag(c * kAC) + 256 * wave, 16, 0, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < P; ++j) ring[j] = stage[afrag(j) + 4 * lane];
+    } else {
+#pragma unroll
+      for (int j = 0; j < P; ++j) ring[j] = a0[afrag(j)];
+    }
   }
   float ld[kRunRG] = {};
   for (int stp = 0; stp < L; ++stp) {
@@ -482,6 +541,7 @@ __global__ __launch_bounds__(64 * kWaves, kRunRG == 2 ? 2 : 1) void k_wide16(
     pad_steps<G, NETS, P>(ring, wl, wn, std::make_integer_sequence<int, LSP - NETS * G::steps()>{});
     if constexpr (!INV && !(CNF_W16_KO & 2)) relayout<G>(st, qs, S, q, X, lane);  // perm then flip
   }
+  if constexpr (G::kLdsA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the block
 
   // slots -> LDS rows -> coalesced stores
   put_state<G>(st, S, X, lane);
@@ -525,6 +585,7 @@ template <int D, int H1, int H2>
 struct G16T {
   using F = G16<D, H1, H2>;
   static constexpr bool kBias = false;
+  static constexpr bool kLdsA = false;
   static constexpr int DT = F::DT, DC = F::DC, NL = F::NL, CT = F::CT, TT = F::TT, XT = F::XT;
   static constexpr int nin(int i) { return F::nout(NL - 1 - i); }
   static constexpr int nout(int i) { return F::nin(NL - 1 - i); }
@@ -1285,7 +1346,7 @@ size_t w16_lds(const Shape& s, int rows = kRows) {
 // forward A-stream floats per layer (pads included: G16::lsp)
 static int64_t w16_la(const WEntry16* e, int nets) {
   const int ls = nets * (e->na / 64);
-  return (int64_t)pad_ls(ls, CNF_W16_FWD_P16) * 64;
+  return (int64_t)pad_fwd(ls) * 64;
 }
 
 static int64_t w16_lt(const WEntry16* e, int nets) {
@@ -1369,7 +1430,9 @@ int wide16_run(const Shape& s, const void* prepared, const float* in, float* out
   const int64_t rows_per_block = (int64_t)kRunRows * kWaves;
   const dim3 grid((unsigned)((B + rows_per_block - 1) / rows_per_block)), block(64 * kWaves);
   WFn fn = e->fn[s.nets - 1][log_priors ? 2 : (inverse ? 1 : 0)];
-  hipLaunchKernelGGL(fn, grid, block, w16_lds(s, kRunRows), st, W, inverse ? inv_q : fwd_q, in, out, ld, B,
+  const size_t lds = CNF_W16_LDSA ? (size_t)(cdiv(kWaves * (kRunRows * (s.D | 1) + s.D), 64) * 64 + 2 * kAC * 64) * 4
+                                  : w16_lds(s, kRunRows);
+  hipLaunchKernelGGL(fn, grid, block, lds, st, W, inverse ? inv_q : fwd_q, in, out, ld, B,
                      s.L, log_priors);
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) {
