@@ -246,6 +246,39 @@ def test_wide_kernel_matches_oracle_and_tile(D, L, hidden, flip, scale):
     assert rel_err(ld.cpu().numpy(), ldt.cpu().numpy()) <= TOL
 
 
+@pytest.mark.parametrize("D,L,hidden", [(100, 2, [100, 100]), (32, 3, [64, 64])])
+@pytest.mark.parametrize("B", [1, 40, 900])
+def test_wide_kernel_partial_blocks(D, L, hidden, B):
+    """k_wide16's last block with waves wholly past the batch (B = 900: one
+    wave of 4 rows, three with none; B = 1, 40: the only block): those waves
+    still take part in the block's LDS copies of the A stream and write
+    nothing.  Forward / inverse against the oracle, predict against the
+    reference formula (calibrators.py:40-44)."""
+    flow = _make_flow(D, L, hidden, 0.05, 5, random_flip=True, scale=True)
+    stack = flow._native_stack()
+    assert stack.kernel_name() == "mfma-wide"
+    x = _logits(B, D, 11)
+    with torch.no_grad():
+        z, ld = flow.transform(x)
+        xr, ild = flow.inverse_transform(z)
+    ol = _oracle_layers(flow)
+    for l, ly in enumerate(flow.layers):
+        ol[l] = O.OracleLayer(D, ol[l].s_net, ol[l].t_net, ly.perm.reshape(-1).cpu().numpy())
+    ozs, old = O.flow_forward(ol, x.cpu().numpy())
+    assert rel_err(z.cpu().numpy(), ozs[-1]) <= TOL
+    # (the reference's log-det squeezes to 0-d at B = 1)
+    assert rel_err(ld.reshape(-1).cpu().numpy(), old.reshape(-1)) <= TOL
+    assert ((xr - x).abs() / (x.abs() + 1)).max().item() <= TOL
+    lp = torch.log_softmax(torch.randn(D, device=x.device), 0)
+    n0 = engine.stats["predict"]
+    probs = stack.predict(x, lp)
+    assert engine.stats["predict"] == n0 + 1  # the fused launch, not the fallback
+    with torch.no_grad():
+        zc, _ = flow.transform(x - x.mean(dim=1, keepdim=True))
+    ref = torch.softmax(torch.log(torch.softmax(zc, 1) + 1e-7) - lp, 1)
+    assert (probs - ref).abs().max().item() <= TOL
+
+
 @pytest.mark.parametrize("name", [n for n in CASES if n != "g6_d4_nan"])
 def test_final_only_inverse_matches_reference_fixture(name):
     """inverse_transform (final x and log-det only -- the cfg5 launch, k_sgpr
