@@ -95,7 +95,10 @@ __host__ __device__ constexpr int pad_ls(int ls, bool p16) {
 #ifndef CNF_W16_LDSA
 #define CNF_W16_LDSA 1
 #endif
-constexpr int kAC = 16;
+#ifndef CNF_W16_LDSA_CHUNK  // steps per LDS chunk (a multiple of 16: one 1-KiB piece per wave per 16)
+#define CNF_W16_LDSA_CHUNK 16
+#endif
+constexpr int kAC = CNF_W16_LDSA_CHUNK;
 #ifndef CNF_W16_LDSA_PMAX  // k_wide16's ring depth with the LDS stream (LDS latency is short)
 #define CNF_W16_LDSA_PMAX 8
 #endif
@@ -184,9 +187,12 @@ __device__ __forceinline__ void refill(float (&ring)[P], const float* __restrict
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         constexpr int S1 = S0 + kAC;  // the next chunk (a = W + layer + 4 lane)
-        const float* src = (S1 < LS ? a + afrag(S1) : an + afrag(S1 - LS)) + 256 * w;
-        __builtin_amdgcn_global_load_lds(const_cast<float*>(src),
-                                         stage + afrag(S1 % (2 * kAC)) + 256 * w, 16, 0, 0);
+#pragma unroll
+        for (int k = 0; k < kAC / 16; ++k) {  // piece k * 4 + w of the chunk's kAC / 4
+          const float* src = (S1 < LS ? a + afrag(S1) : an + afrag(S1 - LS)) + 256 * (4 * k + w);
+          __builtin_amdgcn_global_load_lds(const_cast<float*>(src),
+                                           stage + afrag(S1 % (2 * kAC)) + 256 * (4 * k + w), 16, 0, 0);
+        }
       }
       const v4 v = *reinterpret_cast<const v4*>(stage + afrag(S0 % (2 * kAC)) + 4 * lane);
       ring[(T - 3) % P] = v[0];
@@ -504,9 +510,9 @@ __global__ __launch_bounds__(64 * kWaves, kRunRG == 2 ? 2 : 1) void k_wide16(
     if constexpr (G::kLdsA) {  // chunks 0 and 1 of the first layer, then the ring from LDS
       float* stage = w16_dyn + G::kStateFloats;
 #pragma unroll
-      for (int c = 0; c < 2; ++c)
-        __builtin_amdgcn_global_load_lds(const_cast<float*>(a0 + afrag(c * kAC) + 256 * wave),
-                                         stage + afrag(c * kAC) + 256 * wave, 16, 0, 0);
+      for (int k = 0; k < 2 * kAC / 16; ++k)
+        __builtin_amdgcn_global_load_lds(const_cast<float*>(a0 + 256 * (4 * k + wave)),
+                                         stage + 256 * (4 * k + wave), 16, 0, 0);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
 #pragma unroll
