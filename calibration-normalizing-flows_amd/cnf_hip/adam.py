@@ -28,13 +28,20 @@ def supports(opt):
                    for g in opt.param_groups)
 
 
-def group_lr(torch_adam, stack):
-    """The current learning rate of the param group holding the stack's
-    parameters (an LR scheduler may have changed it since the last step)."""
+def group_hparams(torch_adam, stack):
+    """The CURRENT (lr, betas, eps, weight_decay) of the param group holding
+    the stack's parameters, as Python floats -- a scheduler may have changed
+    any of them since the last step (OneCycleLR and CyclicLR cycle beta1 as
+    well as lr).  None when one of them is a tensor: reading it would sync the
+    host, so the caller hands that group to torch's own optimizer.step()."""
     ids = {id(p) for p in stack.param_tensors()}
     for g in torch_adam.param_groups:
         if any(id(p) in ids for p in g["params"]):
-            return float(g["lr"].item() if torch.is_tensor(g["lr"]) else g["lr"])
+            vals = (g["lr"], g["betas"][0], g["betas"][1], g["eps"], g["weight_decay"])
+            if any(torch.is_tensor(v) for v in vals):
+                return None
+            return (float(g["lr"]), (float(g["betas"][0]), float(g["betas"][1])),
+                    float(g["eps"]), float(g["weight_decay"]))
     raise ValueError("StackAdam: the optimizer holds none of the stack's parameters")
 
 
@@ -79,6 +86,10 @@ class StackAdam:
             self._m = torch.cat([s["exp_avg"].reshape(-1).to(dev, torch.float32) for s in st])
             self._v = torch.cat([s["exp_avg_sq"].reshape(-1).to(dev, torch.float32) for s in st])
         return self
+
+    def set_hparams(self, hp):
+        """Adopt group_hparams()'s (lr, betas, eps, weight_decay)."""
+        self.lr, self.betas, self.eps, self.weight_decay = hp
 
     def store_into(self, torch_adam):
         """Write step count and moments into the torch optimizer's state (the

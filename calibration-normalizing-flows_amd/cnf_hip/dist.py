@@ -117,10 +117,15 @@ class ShardedFlowTrainer:
                            grads_out=buf[:P], terms_out=buf[P:])
             if self.world > 1:
                 dist.all_reduce(buf, group=self.group)
-            from .adam import supports, group_lr
-            if not supports(self.optimizer):
-                # any other optimizer (SGD, AdamW, amsgrad ...) steps itself
-                # on the reduced gradient, as on the CPU path
+            from .adam import supports, group_hparams
+            hp = group_hparams(self.optimizer, stack) if supports(self.optimizer) else None
+            if hp is None:
+                # any other optimizer (SGD, AdamW, amsgrad ...), or tensor-valued
+                # hyper-parameters, steps itself on the reduced gradient, as on
+                # the CPU path (the native moments, if any, go back first)
+                if self._adam is not None:
+                    self._adam.store_into(self.optimizer)
+                    self._adam = None
                 self._set_grads(buf[:P])
                 self.optimizer.step()
                 return buf[P:]
@@ -130,7 +135,9 @@ class ShardedFlowTrainer:
                     # moments and step count over through the torch state
                     self._adam.store_into(self.optimizer)
                 self._adam = StackAdam.like(stack, self.optimizer)
-            self._adam.lr = group_lr(self.optimizer, stack)  # LR schedulers
+            # schedulers may move lr, betas (OneCycleLR / CyclicLR momentum
+            # cycling), eps or weight decay between steps: read all of them
+            self._adam.set_hparams(hp)
             self._adam.step(buf[:P])
             return buf[P:]
         grads, terms = local_loss_and_grads(self.flow, x, y, 1.0 / global_batch, kind, det)

@@ -118,7 +118,8 @@ def _train_pair(opt_fn, sched_fn=None, steps=4, rebuild_at=None):
     return out
 
 
-@pytest.mark.parametrize("name", ["sgd", "adamw", "adam_sched", "adam_rebuild"])
+@pytest.mark.parametrize("name", ["sgd", "adamw", "adam_sched", "adam_onecycle", "adam_tensor_lr",
+                                  "adam_rebuild"])
 def test_trainer_optimizers_match_torch(name):
     if name == "sgd":
         a, b = _train_pair(lambda ps: torch.optim.SGD(ps, lr=0.05, momentum=0.9))
@@ -127,6 +128,15 @@ def test_trainer_optimizers_match_torch(name):
     elif name == "adam_sched":
         a, b = _train_pair(lambda ps: torch.optim.Adam(ps, lr=3e-3),
                            lambda o: torch.optim.lr_scheduler.StepLR(o, 1, gamma=0.3))
+    elif name == "adam_onecycle":
+        # OneCycleLR cycles beta1 as well as lr: the native Adam must follow both
+        a, b = _train_pair(lambda ps: torch.optim.Adam(ps, lr=3e-3),
+                           lambda o: torch.optim.lr_scheduler.OneCycleLR(o, max_lr=1e-2,
+                                                                         total_steps=6),
+                           steps=5)
+    elif name == "adam_tensor_lr":
+        # a tensor lr goes to torch's own step (no host sync on the native path)
+        a, b = _train_pair(lambda ps: torch.optim.Adam(ps, lr=torch.tensor(3e-3), foreach=False))
     else:
         a, b = _train_pair(lambda ps: torch.optim.Adam(ps, lr=3e-3), rebuild_at=2)
     for k in a:

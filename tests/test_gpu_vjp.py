@@ -6,7 +6,7 @@ import torch
 
 from _golden import load, names
 from _model import build_flow
-from cnf_hip import engine
+from cnf_hip import _lib, engine
 from cnf_hip import vjp as V
 from oracle import cnf_oracle as O
 
@@ -21,15 +21,27 @@ def _grad_err(got, ref):
 
 @pytest.mark.parametrize("name", names("g5"))
 @pytest.mark.parametrize("kind", ["cal", "ce"])
-def test_fused_loss_grads_match_reference_autograd(name, kind):
+@pytest.mark.parametrize("via_ops", [False, True])
+def test_fused_loss_grads_match_reference_autograd(name, kind, via_ops):
+    """cnf_loss_vjp through ctypes and through torch.ops.cnf.loss_and_grads.
+    g5_grads_d100_l12 is cfg4's full depth (D=100, L=12, [100,100]): the fused
+    wide sweeps (k_wtrain16_fwd / k_wtrain16_bwd + k_wdw16g) held to the
+    reference's autograd over every layer, no row exemptions."""
     meta, state, d = load(name)
     flow = build_flow(meta, state, DEV)
     stack = flow._native_stack()
     x = torch.from_numpy(d["x"]).to(DEV)
     y = torch.from_numpy(d["y"]).to(DEV)
     B = x.shape[0]
-    terms, grads, _ = V.loss_and_grads(stack, x, y, kind=0 if kind == "cal" else 1, det=1.0,
-                                       grad_scale=1.0 / B)
+    k = 0 if kind == "cal" else 1
+    if via_ops:
+        ops = _lib.torch_ops()
+        if ops is None:
+            pytest.skip("libcnf_torch.so not built")
+        terms, grads = ops.loss_and_grads(x, y, stack.prepared(x.device), stack.desc_ints,
+                                          stack._perms, k, 1.0, 1.0 / B)
+    else:
+        terms, grads, _ = V.loss_and_grads(stack, x, y, kind=k, det=1.0, grad_scale=1.0 / B)
     terms = terms.cpu().numpy()
     ref_loss = float(d["loss_" + kind])
     assert abs(terms[0] / B - ref_loss) / (abs(ref_loss) + 1) <= 1e-5
@@ -178,6 +190,34 @@ def test_wide_vjp_is_deterministic_and_matches_oracle():
                                                for gw, gb in og[l][n]])
                                for l in range(2) for n in ("s", "t")])
         assert _grad_err(gl.cpu().numpy(), flat) <= 1e-4
+
+
+@pytest.mark.parametrize("kind", ["cal", "ce"])
+@pytest.mark.parametrize("path", ["fused", "layerwise"])
+def test_cfg4_depth_grads_and_dx_match_reference(kind, path):
+    """g5_grads_d100_l12 (the reference's autograd at cfg4's full depth):
+    every parameter gradient AND the input gradient of every row, through the
+    fused sweeps (k_wtrain16_fwd / k_wtrain16_bwd + k_wdw16g) and through the
+    layer-at-a-time reverse mode (OPT_NO_WIDE) -- no row exemptions."""
+    meta, state, d = load("g5_grads_d100_l12")
+    flow = build_flow(meta, state, DEV)
+    if path == "layerwise":
+        flow.native_options = _lib.OPT_NO_WIDE
+    stack = flow._native_stack()
+    assert stack.kernel_name() == ("mfma-wide" if path == "fused" else "mfma-tile")
+    x = torch.from_numpy(d["x"]).to(DEV)
+    y = torch.from_numpy(d["y"]).to(DEV)
+    B = x.shape[0]
+    terms, grads, dx = V.loss_and_grads(stack, x, y, kind=0 if kind == "cal" else 1, det=1.0,
+                                        grad_scale=1.0 / B, need_dx=True)
+    ref_loss = float(d["loss_" + kind])
+    assert abs(terms[0].item() / B - ref_loss) / (abs(ref_loss) + 1) <= 1e-5
+    worst = 0.0
+    for (k, p), g in zip([(k, p) for k, p in flow.named_parameters() if p.requires_grad],
+                         V._split(stack, grads)):
+        worst = max(worst, _grad_err(g.cpu().numpy(), d["g%s:%s" % (kind, k)]))
+    assert worst <= 1e-4, worst
+    assert _grad_err(dx.cpu().numpy(), d["dx" + kind]) <= 1e-4
 
 
 def _vjp_ws_bytes(stack, B):

@@ -16,7 +16,7 @@ mode = sys.argv[1] if len(sys.argv) > 1 else "loss"
 opts = int(sys.argv[2]) if len(sys.argv) > 2 else 0
 dev = torch.device("cuda:0")
 rows = []
-for lg in range(16, 24):
+for lg in range(16, 25):
     w = dict(bench.WORKLOADS["cfg2"], B=1 << lg)
     r = bench.Runner(w, dev, 1.0e9, all_outputs=(mode == "all"),
                      mode="loss" if mode == "loss" else "forward")
