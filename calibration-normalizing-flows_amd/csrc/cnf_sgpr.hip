@@ -276,7 +276,11 @@ __device__ __forceinline__ void sp_step(f2 (&v)[P][D], f2 (&ld)[P], SW<SP<D, H1,
       if constexpr (NETS == 1) {  // scale=False: s = 0, exp(0) = 1, log-det += 0
         x = INV ? x - a[p] : x + a[p];
       } else if constexpr (!INV) {
+#ifdef CNF_AB_NO_EXP  // A/B timing only (wrong results): a 4-cycle VALU op per exp
+        x = fmaV(x, a[p] + x, ac.t[p][j]);
+#else
         x = fmaV(x, exp2T(a[p]), ac.t[p][j]);
+#endif
         ld[p] += a[p];
       } else {
         x = (x - ac.t[p][j]) * exp2T(-a[p]);
@@ -340,6 +344,49 @@ __device__ __forceinline__ void pair_loss(const f2* v, f2 ld, uint32_t lab2, int
   for (int q = 0; q < 2; ++q) {
     if (q >= rows) continue;
     const float lpy = zy[q] - (m[q] + __builtin_amdgcn_logf(se[q]) * kLN2);
+    const float l = ld[q];
+    float ce, loss;
+    if (kind == CNF_LOSS_CAL) {
+      ce = -__builtin_amdgcn_logf(__builtin_amdgcn_exp2f(lpy * kL2E) + 1e-7f) * kLN2;
+      loss = ce - l;
+    } else {
+      ce = -lpy;
+      loss = ce - det * l;
+    }
+    if (!ok[q]) ce = loss = __builtin_nanf("");
+    t0 += loss;
+    t1 += ce;
+    t2 += l;
+  }
+}
+
+// pair_loss in two halves for the look-ahead tile loop (kStage 3), so the
+// softmax temporaries are dead before the next tile's rows arrive: the
+// log-sum-exp of both rows from registers first, then -- once the outputs are
+// staged -- z[y] from the LDS tile and the loss terms (same arithmetic, same
+// order as pair_loss<D, 1>).
+template <int D>
+__device__ __forceinline__ f2 pair_lse(const f2* v) {
+  constexpr float kL2E = 1.4426950408889634f, kLN2 = 0.6931471805599453f;
+  f2 m = v[0];
+#pragma unroll
+  for (int j = 1; j < D; ++j) m = maxT(m, v[j]);
+  const f2 nm = m * splat(-kL2E, f2{});
+  f2 se = exp2T(fmaT(kL2E, v[0], nm));
+#pragma unroll
+  for (int j = 1; j < D; ++j) se += exp2T(fmaT(kL2E, v[j], nm));
+  return f2{m[0] + __builtin_amdgcn_logf(se[0]) * kLN2, m[1] + __builtin_amdgcn_logf(se[1]) * kLN2};
+}
+template <int D>
+__device__ __forceinline__ void pair_loss_fin(f2 lse, f2 ld, uint32_t lab2, int kind, float det,
+                                              float& t0, float& t1, float& t2, const float* tile) {
+  const uint32_t b0 = lab2 & 0xffu, b1 = (lab2 >> 8) & 0xffu;
+  const bool ok[2] = {b0 != 0xffu, b1 != 0xffu};
+  constexpr float kL2E = 1.4426950408889634f, kLN2 = 0.6931471805599453f;
+  const float zy[2] = {tile[ok[0] ? (int)b0 : 0], tile[D + (ok[1] ? (int)b1 : 0)]};
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const float lpy = zy[q] - lse[q];
     const float l = ld[q];
     float ce, loss;
     if (kind == CNF_LOSS_CAL) {
@@ -552,11 +599,20 @@ __global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) v
     for (int i = 0; i < slot; ++i) __builtin_amdgcn_s_sleep(CNF_AB_STAGGER);
   }
 #endif
-  if (t < nfull) wave_dma<D, TR>(sm, a.in + (int64_t)t * TF, lane);
-  [[maybe_unused]] float* stg = smem + (kWaves + wv) * TF;  // kStage 2: the output tile
-  f2 pz[kStage == 0 ? P : 1][D], pld[P];
-  int64_t prow = -1;  // first row of the lane's pending (not yet stored) outputs
-  for (; t < nfull; t += nw) {
+#ifdef CNF_AB_NO_MEM  // A/B timing only (wrong results): no input DMA, no label loads, no stores
+  constexpr bool kNoMem = true;
+  a.out = nullptr;
+  a.ld = nullptr;
+#else
+  constexpr bool kNoMem = false;
+#endif
+#ifdef CNF_SGPR_IN_DIRECT
+  constexpr bool kInDirect = P == 1 && (2 * D) % 4 == 0 && kStage == 1;
+#else
+  constexpr bool kInDirect = false;
+#endif
+  if (!kNoMem && !kInDirect && t < nfull) wave_dma<D, TR>(sm, a.in + (int64_t)t * TF, lane);
+  auto set_prio = [&]() {
     --left;  // tiles after this one
 #ifndef CNF_AB_NO_PRIO
     if constexpr (CNF_SGPR_PRIO == 0) {  // longest-remaining first
@@ -573,9 +629,85 @@ __global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) v
       else __builtin_amdgcn_s_setprio(0);
     }
 #endif
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA has landed
+  };
+  if constexpr (kStage == 3) {
+    // One tile of look-ahead through the wave's ONE LDS tile.  The current
+    // tile's rows live in registers while the LDS tile receives the NEXT
+    // tile (its DMA issued a whole tile earlier).  At the boundary: one
+    // vmcnt(0) (everything it covers -- the next rows' DMA, this tile's
+    // labels, the previous tile's stores -- was issued a tile ago), the next
+    // rows move to registers, the LDS tile takes this tile's outputs (LDS
+    // operations of a wave complete in issue order: the staging writes land
+    // after the reads), the outputs leave lane-linear, and the DMA of the
+    // tile after next goes out.
+    static_assert(P == 1, "look-ahead staging carries one pair per lane");
     f2 v[P][D];
-    if constexpr (P == 1) {
+    uint32_t lab = 0;
+    if (t < nfull) {
+      if (!kNoMem) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // first tile landed
+      read_pairs_wait<D>(sm, lane, v);
+      if (!kNoMem && t + nw < nfull) wave_dma<D, TR>(sm, a.in + (int64_t)(t + nw) * TF, lane);
+      if constexpr (MODE == kLoss)
+        if (!kNoMem) lab = load_labels<D, P>(a.y + (int64_t)t * TR + 2 * P * lane, 2 * P, y16);
+    }
+    for (; t < nfull; t += nw) {
+      set_prio();
+#ifdef CNF_SGPR_TRACE
+      if (ntr < 2) CNF_TR(1 + 2 * ntr);
+#endif
+      const int64_t row0 = (int64_t)t * TR;
+      const bool more = t + nw < nfull;
+      f2 ld[P];
+      compute(v, ld, row0, 2 * P);
+      [[maybe_unused]] f2 lse;
+      if constexpr (MODE == kLoss) lse = pair_lse<D>(v[0]);
+      __builtin_amdgcn_sched_barrier(0);  // no compute below the next rows' arrival
+      // the lane index laundered per tile: per-lane 64-bit addresses are formed
+      // here, not hoisted out of the loop and carried (spilled) across compute
+      int ln = lane;
+      asm volatile("" : "+v"(ln));
+      if (!kNoMem) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      f2 vn[P][D];
+      if (more) read_pairs_wait<D>(sm, ln, vn);
+      if constexpr (MODE == kLoss) {
+        stage_pairs<D, P>(sm, ln, v);
+        pair_loss_fin<D>(lse, ld[0], lab, a.kind, a.det, lt0, lt1, lt2, sm + 2 * D * ln);
+      }
+#ifdef CNF_SGPR_TRACE
+      if (ntr < 2) CNF_TR(2 + 2 * ntr);
+      CNF_TR(5);
+      ++ntr;
+#endif
+      if (a.out) {
+        if constexpr (MODE != kLoss) stage_pairs<D, P>(sm, ln, v);
+        store_tile<TF>(a.out + row0 * D, sm, ln);
+      }
+      if (a.ld) store_lds<P>(a.ld + row0 + 2 * P * ln, ld, 2 * P, al_ld);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // staged tile read back
+      if (!kNoMem && t + 2 * nw < nfull)
+        wave_dma<D, TR>(sm, a.in + (int64_t)(t + 2 * nw) * TF, ln);
+      if constexpr (MODE == kLoss)
+        if (!kNoMem && more) lab = load_labels<D, P>(a.y + row0 + (int64_t)nw * TR + 2 * P * ln,
+                                                     2 * P, y16);
+      if (more) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) v[0][k] = vn[0][k];
+      }
+    }
+  }
+  [[maybe_unused]] float* stg = smem + (kWaves + wv) * TF;  // kStage 2: the output tile
+  f2 pz[kStage == 0 ? P : 1][D], pld[P];
+  int64_t prow = -1;  // first row of the lane's pending (not yet stored) outputs
+  for (; kStage != 3 && t < nfull; t += nw) {
+    set_prio();
+    f2 v[P][D];
+    if constexpr (kInDirect) {
+      if constexpr (P == 1) load_pairs_direct<D>(a.in + ((int64_t)t * TR + 2 * lane) * D, v);
+    } else if (!kNoMem) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA has landed
+    }
+    if constexpr (kInDirect) {
+    } else if constexpr (P == 1) {
       read_pairs_wait<D>(sm, lane, v);  // rows are in registers
     } else {
       read_pairs<D, P>(sm, lane, v);
@@ -595,7 +727,8 @@ __global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) v
     }
     if (kStage != 1 && t + nw < nfull) wave_dma<D, TR>(sm, a.in + (int64_t)(t + nw) * TF, lane);
     uint32_t lab = 0;
-    if constexpr (MODE == kLoss) lab = load_labels<D, P>(a.y + row0 + 2 * P * lane, 2 * P, y16);
+    if constexpr (MODE == kLoss)
+      if (!kNoMem) lab = load_labels<D, P>(a.y + row0 + 2 * P * lane, 2 * P, y16);
     f2 ld[P];
     compute(v, ld, row0, 2 * P);
     if constexpr (MODE == kLoss) {
@@ -621,7 +754,8 @@ __global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) v
       }
       if (a.ld) store_lds<P>(a.ld + row0 + 2 * P * lane, ld, 2 * P, al_ld);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (t + nw < nfull) wave_dma<D, TR>(sm, a.in + (int64_t)(t + nw) * TF, lane);
+      if (!kNoMem && !kInDirect && t + nw < nfull)
+        wave_dma<D, TR>(sm, a.in + (int64_t)(t + nw) * TF, lane);
     } else {
       if constexpr (kStage == 0) {
 #pragma unroll

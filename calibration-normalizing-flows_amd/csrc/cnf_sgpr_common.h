@@ -130,6 +130,15 @@ __device__ __forceinline__ void sissue(SW<NC>& r, const float* p) {
 
 // HBM -> LDS copy of one full wave tile (TR*D floats, 16-B aligned) by
 // LDS-DMA: one global_load_lds_dwordx4 moves 1 KiB, lane-linear.
+// CNF_SGPR_DMA_AUX: the loads' cache-policy bits (gfx950: 1 sc0, 2 nt, 16
+// sc1).  Streaming (nt) input: the cfg2 pass is held at the board's power cap
+// (1.4 kW at 2^23 rows; tools/power_probe.py), and the nt DMA takes 8 % less
+// energy per row than the default policy -- 31.39 -> 30.24 us per 2^20-row
+// loss call, 192.8 -> 188.9 us at 2^23, outputs bitwise unchanged (round 5,
+// profiles/r05_ab_power.jsonl); sc1 nt measured the same as nt.
+#ifndef CNF_SGPR_DMA_AUX
+#define CNF_SGPR_DMA_AUX 2
+#endif
 template <int D, int TR>
 __device__ __forceinline__ void wave_dma(float* sm, const float* __restrict__ src, int lane) {
   constexpr int N4 = TR * D / 4, NI = (N4 + 63) / 64;
@@ -138,8 +147,29 @@ __device__ __forceinline__ void wave_dma(float* sm, const float* __restrict__ sr
     if (N4 % 64 == 0 || i * 64 + lane < N4)
       __builtin_amdgcn_global_load_lds(src + (i * 64 + lane) * 4,
                                        (__attribute__((address_space(3))) void*)(sm + i * 256), 16,
-                                       0, 0);
+                                       0, CNF_SGPR_DMA_AUX);
   }
+}
+
+// A/B (CNF_SGPR_IN_DIRECT): the lane's two rows (2*D contiguous floats, 16-B
+// aligned when D is even) straight from HBM into registers by 16-B loads,
+// no LDS hop; the compiler's vmcnt wait guards the first use.
+template <int D>
+__device__ __forceinline__ void load_pairs_direct(const float* __restrict__ src, f2 (&v)[1][D]) {
+  static_assert((2 * D) % 4 == 0, "direct row loads need 16-B pairs");
+  using v4 = __attribute__((ext_vector_type(4))) float;
+  float f[2 * D];
+#pragma unroll
+  for (int i = 0; i < D / 2; ++i) {
+#ifdef CNF_SGPR_IN_NT
+    const v4 q = __builtin_nontemporal_load(reinterpret_cast<const v4*>(src) + i);
+#else
+    const v4 q = reinterpret_cast<const v4*>(src)[i];
+#endif
+    f[4 * i] = q.x, f[4 * i + 1] = q.y, f[4 * i + 2] = q.z, f[4 * i + 3] = q.w;
+  }
+#pragma unroll
+  for (int k = 0; k < D; ++k) v[0][k] = f2{f[k], f[D + k]};
 }
 
 // the lane's pairs from the LDS tile (one ds_read2_b32 per feature and pair)
@@ -259,7 +289,13 @@ __device__ __forceinline__ void store_lds(float* __restrict__ dst, const f2 (&ld
     *reinterpret_cast<float4*>(dst) = float4{ld[0].x, ld[0].y, ld[P - 1].x, ld[P - 1].y};
   } else if (rows == 2 * P && al >= 8) {
 #pragma unroll
-    for (int p = 0; p < P; ++p) reinterpret_cast<float2*>(dst)[p] = float2{ld[p].x, ld[p].y};
+    for (int p = 0; p < P; ++p) {
+#ifdef CNF_SGPR_LD_NT  // A/B: streaming log-det stores
+      __builtin_nontemporal_store(ld[p], reinterpret_cast<f2*>(dst) + p);
+#else
+      reinterpret_cast<float2*>(dst)[p] = float2{ld[p].x, ld[p].y};
+#endif
+    }
   } else {
 #pragma unroll
     for (int p = 0; p < P; ++p) {
@@ -294,7 +330,12 @@ __device__ __forceinline__ uint32_t load_labels(const int64_t* __restrict__ y, i
   for (int p = 0; p < P; ++p) {
     int lo0 = 0, hi0 = 0, lo1 = 0, hi1 = 0;
     if (rows == 2 * P && al16) {
+#ifdef CNF_SGPR_LAB_NT  // A/B: streaming label loads
+      using v4i = __attribute__((ext_vector_type(4))) int;
+      const v4i q = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(y32) + p);
+#else
       const int4 q = reinterpret_cast<const int4*>(y32)[p];
+#endif
       lo0 = q.x, hi0 = q.y, lo1 = q.z, hi1 = q.w;
     } else {
       if (2 * p < rows) lo0 = y32[4 * p], hi0 = y32[4 * p + 1];

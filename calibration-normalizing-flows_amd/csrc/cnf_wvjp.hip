@@ -1273,12 +1273,15 @@ void gemm(GemmArgs ga, int64_t B, int cols, int K, int nz, bool bt, int epi, boo
 bool wvjp_ok(const Shape& s) {
   if (s.strict && (s.alt_mask || s.s_tanh)) return false;
   constexpr size_t kLds = 160 * 1024;
+  // column counts as the launches use them: a strict stack's last Linear
+  // writes all D columns, and its first-Linear back-prop produces all D
+  // input columns (x_b = mask * x), not DT / DC
   for (int k = 0; k < s.n_lin; ++k) {
-    const int cols = k == s.n_lin - 1 ? s.DT : hp(s, k);
+    const int cols = k == s.n_lin - 1 ? lin_out(s, k) : hp(s, k);
     if (gemm_lds(cols, lin_in(s, k), false) > kLds) return false;               // forward
     if (k > 0 && gemm_lds(gp(s, k - 1), lin_out(s, k), false) > kLds) return false;  // back-prop
   }
-  return gemm_lds(s.DC, lin_out(s, 0), s.nets == 2) <= kLds;
+  return gemm_lds(s.strict ? s.D : s.DC, lin_out(s, 0), s.nets == 2) <= kLds;
 }
 
 namespace {

@@ -220,8 +220,9 @@ def test_fused_forward_loss_matches_oracle(kind):
     (32, 4, [64, 64], True, True),       # mid width, one partial state tile
 ])
 def test_wide_kernel_matches_oracle_and_tile(D, L, hidden, flip, scale):
-    """k_wide (cnf_wide.hip): register-resident MFMA path against the numpy
-    oracle, the round trip, and the LDS-tile kernel it replaces."""
+    """k_wide16 (cnf_wide16.hip, 16x16x4 register tiles): register-resident
+    MFMA path against the numpy oracle, the round trip, and the LDS-tile
+    kernel (k_tile) it replaces."""
     flow = _make_flow(D, L, hidden, 0.05, 21, random_flip=flip, scale=scale)
     assert flow._native_stack().kernel_name() == "mfma-wide"
     x = _logits(1000, D, 3)                     # ragged: 31 full waves + 8 rows

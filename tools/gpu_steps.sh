@@ -11,7 +11,12 @@
 #   ab           tools/quick_rate.py $AB_MODE for every tools/ab/lib*.so (make ab)
 #   train        cfg2 / cfg4 fused training-step times (bench.train_step_rate)
 #   wide         cfg4 forward (k_wide) time
+#   sweep        tools/batch_sweep.py loss / forward (2^16..2^24 rows)
+#   mix          tools/ubench/mix_rate (VALU / MFMA co-issue rates)
 #   calib        the calibrator-fit epoch variant (bench.calibrator_epoch_rate)
+#   abbits       tools/ab/ab_bits.py (output fingerprints) for the shipped lib and every tools/ab/lib*.so
+#   abtrace      tools/sgpr_trace.py for every tools/ab/lib*.so (trace builds) at AB_TRACE_B rows
+#   abpower      tools/power_probe.py (board power, energy per row) for the shipped lib and every tools/ab/lib*.so
 #   abterms      tools/ab/ab_terms.py (loss-term bits + fp64 check) for every tools/ab/lib*.so
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -35,12 +40,36 @@ for step in "$@"; do
     rate) run rate 300 python tools/quick_rate.py loss forward inverse ;;
     train) run train 300 python -c "import json, torch, bench; d = torch.device('cuda:0'); print(json.dumps({w: bench.train_step_rate(d, w, steps=(20 if w == 'cfg2' else 5)) for w in ('cfg2', 'cfg4')}))" ;;
     wide) run wide 300 python -c "import json, torch, bench; d = torch.device('cuda:0'); r = bench.Runner(dict(bench.WORKLOADS['cfg4']), d, 1e9); t = min(bench.kernel_only_seconds(r, 10) for _ in range(3)); print(json.dumps({'cfg4_forward_us': round(t * 1e6, 1)}))" ;;
+    sweep) run sweep_loss 300 python tools/batch_sweep.py loss && run sweep_fwd 300 python tools/batch_sweep.py forward ;;
+    mix) run mix_rate 120 tools/ubench/mix_rate ;;
     calib) run calib 300 python -c "import json, torch, bench; print(json.dumps(bench.calibrator_epoch_rate(torch.device('cuda:0'))))" ;;
     ab)
       for lib in tools/ab/lib*.so; do
         [ -e "$lib" ] || continue
         n=$(basename "$lib" .so)
         TAILN=${AB_TAIL:-4} CNF_HIP_LIB=$PWD/$lib run "ab_$n" 300 python tools/quick_rate.py ${AB_MODE:-loss}
+      done ;;
+    abbits)
+      run abbits_shipped 300 python tools/ab/ab_bits.py
+      for lib in tools/ab/lib*.so; do
+        [ -e "$lib" ] || continue
+        n=$(basename "$lib" .so)
+        CNF_HIP_LIB=$PWD/$lib run "abbits_$n" 300 python tools/ab/ab_bits.py
+      done ;;
+    abtrace)
+      for lib in tools/ab/lib*.so; do
+        [ -e "$lib" ] || continue
+        n=$(basename "$lib" .so)
+        for b in ${AB_TRACE_B:-1048576 8388608}; do
+          TAILN=1 CNF_HIP_LIB=$PWD/$lib run "abtrace_${n}_$b" 180 python tools/sgpr_trace.py ${AB_MODE:-loss} $b
+        done
+      done ;;
+    abpower)
+      TAILN=1 run power_shipped 120 python tools/power_probe.py ${AB_MODE:-loss} 3 ${AB_B:-1048576}
+      for lib in tools/ab/lib*.so; do
+        [ -e "$lib" ] || continue
+        n=$(basename "$lib" .so)
+        TAILN=1 CNF_HIP_LIB=$PWD/$lib run "power_$n" 120 python tools/power_probe.py ${AB_MODE:-loss} 3 ${AB_B:-1048576}
       done ;;
     abterms)
       for lib in tools/ab/lib*.so; do
