@@ -86,10 +86,16 @@ def _coupling_params(flow):
 class ShardedFlowTrainer:
     """Data-parallel trainer for a Flow of NvpCouplingLayers."""
 
-    def __init__(self, flow, optimizer, group=None, broadcast=True):
+    def __init__(self, flow, optimizer, group=None, broadcast=True, nan_guard=False):
         self.flow = flow
         self.optimizer = optimizer
         self.group = group
+        # nan_guard: every native step also ORs the non-finite state of the
+        # reduced [grads | loss terms] buffer into self.guard.flag (device int,
+        # no host sync; the reference aborts its loop on NaN predictions,
+        # run_experiment3D.py:129-131 -- read self.guard.tripped() when wanted)
+        self.nan_guard = nan_guard
+        self.guard = None
         self.params = list(_coupling_params(flow))
         self._adam = None  # StackAdam of the native path (built on the first step)
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -117,6 +123,11 @@ class ShardedFlowTrainer:
                            grads_out=buf[:P], terms_out=buf[P:])
             if self.world > 1:
                 dist.all_reduce(buf, group=self.group)
+            if self.nan_guard:
+                if self.guard is None:
+                    from .guard import NonFiniteGuard
+                    self.guard = NonFiniteGuard(x.device)
+                self.guard.check(buf)
             from .adam import supports, group_hparams
             hp = group_hparams(self.optimizer, stack) if supports(self.optimizer) else None
             if hp is None:

@@ -293,9 +293,9 @@ class CouplingStack:
     def forward_autograd(self, x, want_all):
         """Forward with gradients w.r.t. x and every parameter (cnf_vjp): the
         cnf::flow operator (autograd kernel in C++) or the Python Function.
-        Stacks without a native reverse mode (strict_nan) take the Python
-        Function, whose backward falls back to torch autograd (vjp._torch_vjp);
-        the C++ kernel would raise there."""
+        Stacks whose reverse mode the ABI reports unsupported (legacy strict
+        options) take the Python Function, whose backward falls back to torch
+        autograd (vjp._torch_vjp); the C++ kernel would raise there."""
         ps = self.param_tensors()
         ops = _ops()
         if ops is not None and self.has_native_vjp():
@@ -308,7 +308,7 @@ class CouplingStack:
 
 
     def has_native_vjp_inverse(self):
-        """True when cnf_vjp_inverse serves this descriptor (not strict_nan)."""
+        """True when cnf_vjp_inverse serves this descriptor (strict_nan included)."""
         if self._vjp_inv_ok is None:
             n = ctypes.c_size_t()
             st = _lib.lib().cnf_vjp_inverse_workspace_bytes(ctypes.byref(self.desc),

@@ -153,9 +153,9 @@ _warned = set()
 
 def _torch_vjp(stack, x, g_out, g_ld, all_grads, need_dx):
     """Reverse modes the ABI reports unsupported (CNF_ERR_UNSUPPORTED: shapes
-    past the layer-at-a-time kernels' LDS envelope, and the strict_nan
-    inverse's reverse mode): autograd through the layers' own torch ops, on
-    the same device.  The strict_nan FORWARD reverse mode is native."""
+    past the layer-at-a-time kernels' LDS envelope): autograd through the
+    layers' own torch ops, on the same device.  strict_nan stacks have native
+    reverse modes for the forward and the inverse."""
     key = (stack.dim, tuple(stack.hidden), stack.strict_nan)
     if stack.options & (_lib.OPT_ALT_MASK | _lib.OPT_S_TANH):
         # _torch_forward restates the maintained (ReLU, data-flip) layer only:

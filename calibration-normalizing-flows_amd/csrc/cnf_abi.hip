@@ -295,7 +295,6 @@ int cnf_vjp_inverse_workspace_bytes(const cnf_desc* desc, int64_t B, size_t* byt
   if (st != CNF_OK) return st;
   if (!bytes) return CNF_ERR_NULL;
   if (B < 0) return CNF_ERR_BATCH;
-  if (s.strict) return CNF_ERR_UNSUPPORTED;  // strict: the forward's reverse mode only
   return wvjp_inv_workspace(s, B, bytes);
 }
 

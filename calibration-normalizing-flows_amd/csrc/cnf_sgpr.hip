@@ -301,6 +301,34 @@ __device__ __forceinline__ void sp_step(f2 (&v)[P][D], f2 (&ld)[P], SW<SP<D, H1,
 // tile I/O: a lane's 2P rows (pairs p = rows 2P*l + 2p, +1) are the 2*P*D
 // contiguous floats at row 2P*l of the wave's tile
 // ---------------------------------------------------------------------------
+// max over a row of the pair (q = 0 / 1) by v_max3_f32 (max is exact in any
+// order; the fmaxf chain also canonicalised NaNs: 14 instead of 10 VALU per
+// pair at D=10)
+__device__ __forceinline__ float max3f(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ float max2f(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+template <int D>
+__device__ __forceinline__ f2 pair_max(const f2* v) {
+  f2 m;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    float r = v[0][q];
+    int j = 1;
+#pragma unroll
+    for (; j + 1 < D; j += 2) r = max3f(r, v[j][q], v[j + 1][q]);
+    if (j < D) r = max2f(r, v[j][q]);
+    m[q] = r;
+  }
+  return m;
+}
+
 // Loss terms of one pair's rows (logical order):
 // CAL: loss = -(log(softmax(z)[y] + 1e-7) + ld)    calibrators.py:288-291
 // CE:  loss = -log_softmax(z)[y] - det * ld         run_experiment3D.py:107
@@ -323,9 +351,7 @@ __device__ __forceinline__ void pair_loss(const f2* v, f2 ld, uint32_t lab2, int
     zy[0] = tile[0];
     zy[1] = tile[1];
   }
-  f2 m = v[0];
-#pragma unroll
-  for (int j = 1; j < D; ++j) m = maxT(m, v[j]);
+  const f2 m = pair_max<D>(v);
   const f2 nm = m * splat(-kL2E, f2{});
   f2 se = exp2T(fmaT(kL2E, v[0], nm));
 #pragma unroll
@@ -360,56 +386,14 @@ __device__ __forceinline__ void pair_loss(const f2* v, f2 ld, uint32_t lab2, int
   }
 }
 
-// pair_loss in two halves for the look-ahead tile loop (kStage 3), so the
-// softmax temporaries are dead before the next tile's rows arrive: the
-// log-sum-exp of both rows from registers first, then -- once the outputs are
-// staged -- z[y] from the LDS tile and the loss terms (same arithmetic, same
-// order as pair_loss<D, 1>).
-template <int D>
-__device__ __forceinline__ f2 pair_lse(const f2* v) {
-  constexpr float kL2E = 1.4426950408889634f, kLN2 = 0.6931471805599453f;
-  f2 m = v[0];
-#pragma unroll
-  for (int j = 1; j < D; ++j) m = maxT(m, v[j]);
-  const f2 nm = m * splat(-kL2E, f2{});
-  f2 se = exp2T(fmaT(kL2E, v[0], nm));
-#pragma unroll
-  for (int j = 1; j < D; ++j) se += exp2T(fmaT(kL2E, v[j], nm));
-  return f2{m[0] + __builtin_amdgcn_logf(se[0]) * kLN2, m[1] + __builtin_amdgcn_logf(se[1]) * kLN2};
-}
-template <int D>
-__device__ __forceinline__ void pair_loss_fin(f2 lse, f2 ld, uint32_t lab2, int kind, float det,
-                                              float& t0, float& t1, float& t2, const float* tile) {
-  const uint32_t b0 = lab2 & 0xffu, b1 = (lab2 >> 8) & 0xffu;
-  const bool ok[2] = {b0 != 0xffu, b1 != 0xffu};
-  constexpr float kL2E = 1.4426950408889634f, kLN2 = 0.6931471805599453f;
-  const float zy[2] = {tile[ok[0] ? (int)b0 : 0], tile[D + (ok[1] ? (int)b1 : 0)]};
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const float lpy = zy[q] - lse[q];
-    const float l = ld[q];
-    float ce, loss;
-    if (kind == CNF_LOSS_CAL) {
-      ce = -__builtin_amdgcn_logf(__builtin_amdgcn_exp2f(lpy * kL2E) + 1e-7f) * kLN2;
-      loss = ce - l;
-    } else {
-      ce = -lpy;
-      loss = ce - det * l;
-    }
-    if (!ok[q]) ce = loss = __builtin_nanf("");
-    t0 += loss;
-    t1 += ce;
-    t2 += l;
-  }
-}
-
 // x - mean(x) per row (the calibrator centres logits before the flow,
 // calibrators.py:17,42)
-template <int D>
+// (O: the row is held reversed; the sum runs in logical order either way)
+template <int D, bool O>
 __device__ __forceinline__ void centre(f2* v) {
-  f2 s = v[0];
+  f2 s = v[R<D, O>(0)];
 #pragma unroll
-  for (int j = 1; j < D; ++j) s += v[j];
+  for (int j = 1; j < D; ++j) s += v[R<D, O>(j)];
   const f2 mu = s * splat(1.f / D, f2{});
 #pragma unroll
   for (int j = 0; j < D; ++j) v[j] -= mu;
@@ -420,9 +404,7 @@ __device__ __forceinline__ void centre(f2* v) {
 template <int D>
 __device__ __forceinline__ void pair_predict(f2* v, const float* __restrict__ lp) {
   constexpr float kL2E = 1.4426950408889634f, kLN2 = 0.6931471805599453f;
-  f2 m = v[0];
-#pragma unroll
-  for (int j = 1; j < D; ++j) m = maxT(m, v[j]);
+  const f2 m = pair_max<D>(v);
   const f2 nm = m * splat(-kL2E, f2{});
   f2 e[D], se = splat(0.f, f2{});
 #pragma unroll
@@ -438,9 +420,7 @@ __device__ __forceinline__ void pair_predict(f2* v, const float* __restrict__ lp
     a[j] = f2{__builtin_amdgcn_logf(p.x), __builtin_amdgcn_logf(p.y)} * splat(kLN2, f2{}) -
            splat(lp[j], f2{});
   }
-  f2 m2 = a[0];
-#pragma unroll
-  for (int j = 1; j < D; ++j) m2 = maxT(m2, a[j]);
+  const f2 m2 = pair_max<D>(a);
   const f2 nm2 = m2 * splat(-kL2E, f2{});
   f2 s2 = splat(0.f, f2{});
 #pragma unroll
@@ -511,12 +491,20 @@ __global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) v
   }
   float lt0 = 0.f, lt1 = 0.f, lt2 = 0.f;
 
-  // One tile's compute: rows in v (orientation 0) -> outputs in v (logical
-  // order), log-det in ld; every-layer stores on the way (rows valid: nr).
+  // One tile's compute: rows in v -> outputs in v (logical order), log-det in
+  // ld; every-layer stores on the way (rows valid: nr).  An odd stack's lone
+  // layer runs FIRST, on a row read reversed (orientation 1: the tile loads
+  // below write v[D-1-k] for feature k), so every stack leaves the layer-pair
+  // loop in logical order: no unflip, and no register shuffle where the odd
+  // and even paths meet (16 v_mov_b64 per tile when the lone layer ran last).
+  const bool odd = (L & 1) != 0;
   auto compute = [&](f2 (&v)[P][D], f2 (&ld)[P], int64_t row0, int nr) {
 #pragma unroll
     for (int p = 0; p < P; ++p) {
-      if constexpr (MODE == kPredict) centre<D>(v[p]);
+      if constexpr (MODE == kPredict) {
+        if (odd) centre<D, true>(v[p]);
+        else centre<D, false>(v[p]);
+      }
       ld[p] = splat(0.f, f2{});
     }
     auto st_all = [&](int i, auto O_) {
@@ -531,6 +519,20 @@ __global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) v
       }
     };
     int i = 0;
+    if (odd) {  // orientation 1 in, 0 out
+      const int la = layer_of(0);
+      const bool pa = PERM && (lflag[la] & kFlagPerm);
+      const float* wa = W + (int64_t)la * LF;
+      SW<S::NC> cur, alt;
+      // a layer entered in orientation 1 starts on buffer parity NETS * NL
+      // (sp_step's O): its first block goes to that buffer
+      if constexpr (((NETS * S::NL) & 1) != 0) sissue(alt, wa + lin_at<S, NETS, 0>());
+      else sissue(cur, wa + lin_at<S, NETS, 0>());
+      sp_step<D, H1, H2, INV, true, NETS, PERM, false, P>(v, ld, cur, alt, wa, nullptr, pa,
+                                                          qtab + la * D);
+      st_all(0, std::false_type{});
+      i = 1;
+    }
     for (; i + 1 < L; i += 2) {
       const int la = layer_of(i), lb = layer_of(i + 1);
       const bool pa = PERM && (lflag[la] & kFlagPerm);
@@ -545,18 +547,6 @@ __global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) v
       sp_step<D, H1, H2, INV, true, NETS, PERM, false, P>(v, ld, cur, alt, wb, nullptr, pb,
                                                           qtab + lb * D);
       st_all(i + 1, std::false_type{});
-    }
-    if (i < L) {
-      const int la = layer_of(i);
-      const bool pa = PERM && (lflag[la] & kFlagPerm);
-      const float* wa = W + (int64_t)la * LF;
-      SW<S::NC> cur, alt;
-      sissue(cur, wa + lin_at<S, NETS, 0>());
-      sp_step<D, H1, H2, INV, false, NETS, PERM, false, P>(v, ld, cur, alt, wa, nullptr, pa,
-                                                           qtab + la * D);
-      st_all(i, std::true_type{});
-#pragma unroll
-      for (int p = 0; p < P; ++p) unflip<D>(v[p]);
     }
 #pragma unroll
     for (int p = 0; p < P; ++p) {
@@ -576,6 +566,9 @@ __global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) v
     }
   };
 
+#ifdef CNF_AB_VGPR80  // A/B: the forward variant forced to >= 80 VGPRs (dispatch-spread test)
+  if constexpr (MODE == kFwd) asm volatile("v_mov_b32 v79, 0" ::: "v79");
+#endif
   // -------- full tiles: LDS-DMA in, deferred 16-B stores out --------
   CNF_TR(0);
   CNF_TRC(0);
@@ -606,12 +599,7 @@ __global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) v
 #else
   constexpr bool kNoMem = false;
 #endif
-#ifdef CNF_SGPR_IN_DIRECT
-  constexpr bool kInDirect = P == 1 && (2 * D) % 4 == 0 && kStage == 1;
-#else
-  constexpr bool kInDirect = false;
-#endif
-  if (!kNoMem && !kInDirect && t < nfull) wave_dma<D, TR>(sm, a.in + (int64_t)t * TF, lane);
+  if (!kNoMem && t < nfull) wave_dma<D, TR>(sm, a.in + (int64_t)t * TF, lane);
   auto set_prio = [&]() {
     --left;  // tiles after this one
 #ifndef CNF_AB_NO_PRIO
@@ -630,87 +618,19 @@ __global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) v
     }
 #endif
   };
-  if constexpr (kStage == 3) {
-    // One tile of look-ahead through the wave's ONE LDS tile.  The current
-    // tile's rows live in registers while the LDS tile receives the NEXT
-    // tile (its DMA issued a whole tile earlier).  At the boundary: one
-    // vmcnt(0) (everything it covers -- the next rows' DMA, this tile's
-    // labels, the previous tile's stores -- was issued a tile ago), the next
-    // rows move to registers, the LDS tile takes this tile's outputs (LDS
-    // operations of a wave complete in issue order: the staging writes land
-    // after the reads), the outputs leave lane-linear, and the DMA of the
-    // tile after next goes out.
-    static_assert(P == 1, "look-ahead staging carries one pair per lane");
-    f2 v[P][D];
-    uint32_t lab = 0;
-    if (t < nfull) {
-      if (!kNoMem) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // first tile landed
-      read_pairs_wait<D>(sm, lane, v);
-      if (!kNoMem && t + nw < nfull) wave_dma<D, TR>(sm, a.in + (int64_t)(t + nw) * TF, lane);
-      if constexpr (MODE == kLoss)
-        if (!kNoMem) lab = load_labels<D, P>(a.y + (int64_t)t * TR + 2 * P * lane, 2 * P, y16);
-    }
-    for (; t < nfull; t += nw) {
-      set_prio();
-#ifdef CNF_SGPR_TRACE
-      if (ntr < 2) CNF_TR(1 + 2 * ntr);
-#endif
-      const int64_t row0 = (int64_t)t * TR;
-      const bool more = t + nw < nfull;
-      f2 ld[P];
-      compute(v, ld, row0, 2 * P);
-      [[maybe_unused]] f2 lse;
-      if constexpr (MODE == kLoss) lse = pair_lse<D>(v[0]);
-      __builtin_amdgcn_sched_barrier(0);  // no compute below the next rows' arrival
-      // the lane index laundered per tile: per-lane 64-bit addresses are formed
-      // here, not hoisted out of the loop and carried (spilled) across compute
-      int ln = lane;
-      asm volatile("" : "+v"(ln));
-      if (!kNoMem) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      f2 vn[P][D];
-      if (more) read_pairs_wait<D>(sm, ln, vn);
-      if constexpr (MODE == kLoss) {
-        stage_pairs<D, P>(sm, ln, v);
-        pair_loss_fin<D>(lse, ld[0], lab, a.kind, a.det, lt0, lt1, lt2, sm + 2 * D * ln);
-      }
-#ifdef CNF_SGPR_TRACE
-      if (ntr < 2) CNF_TR(2 + 2 * ntr);
-      CNF_TR(5);
-      ++ntr;
-#endif
-      if (a.out) {
-        if constexpr (MODE != kLoss) stage_pairs<D, P>(sm, ln, v);
-        store_tile<TF>(a.out + row0 * D, sm, ln);
-      }
-      if (a.ld) store_lds<P>(a.ld + row0 + 2 * P * ln, ld, 2 * P, al_ld);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // staged tile read back
-      if (!kNoMem && t + 2 * nw < nfull)
-        wave_dma<D, TR>(sm, a.in + (int64_t)(t + 2 * nw) * TF, ln);
-      if constexpr (MODE == kLoss)
-        if (!kNoMem && more) lab = load_labels<D, P>(a.y + row0 + (int64_t)nw * TR + 2 * P * ln,
-                                                     2 * P, y16);
-      if (more) {
-#pragma unroll
-        for (int k = 0; k < D; ++k) v[0][k] = vn[0][k];
-      }
-    }
-  }
   [[maybe_unused]] float* stg = smem + (kWaves + wv) * TF;  // kStage 2: the output tile
   f2 pz[kStage == 0 ? P : 1][D], pld[P];
   int64_t prow = -1;  // first row of the lane's pending (not yet stored) outputs
-  for (; kStage != 3 && t < nfull; t += nw) {
+  for (; t < nfull; t += nw) {
     set_prio();
+    if (!kNoMem) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA has landed
     f2 v[P][D];
-    if constexpr (kInDirect) {
-      if constexpr (P == 1) load_pairs_direct<D>(a.in + ((int64_t)t * TR + 2 * lane) * D, v);
-    } else if (!kNoMem) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA has landed
-    }
-    if constexpr (kInDirect) {
-    } else if constexpr (P == 1) {
-      read_pairs_wait<D>(sm, lane, v);  // rows are in registers
+    if constexpr (P == 1) {  // rows are in registers (reversed for an odd stack)
+      if (odd) read_pairs_wait<D, true>(sm, lane, v);
+      else read_pairs_wait<D, false>(sm, lane, v);
     } else {
-      read_pairs<D, P>(sm, lane, v);
+      if (odd) read_pairs<D, P, true>(sm, lane, v);
+      else read_pairs<D, P, false>(sm, lane, v);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
 #ifdef CNF_SGPR_TRACE
@@ -754,8 +674,7 @@ __global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) v
       }
       if (a.ld) store_lds<P>(a.ld + row0 + 2 * P * lane, ld, 2 * P, al_ld);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (!kNoMem && !kInDirect && t + nw < nfull)
-        wave_dma<D, TR>(sm, a.in + (int64_t)(t + nw) * TF, lane);
+      if (!kNoMem && t + nw < nfull) wave_dma<D, TR>(sm, a.in + (int64_t)(t + nw) * TF, lane);
     } else {
       if constexpr (kStage == 0) {
 #pragma unroll
@@ -785,13 +704,18 @@ __global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) v
     const int64_t left_rows = B - r;
     const int nr = left_rows <= 0 ? 0 : (left_rows >= 2 * P ? 2 * P : (int)left_rows);
     f2 v[P][D];
+    auto load_rows = [&](auto O_) {
+      constexpr bool O = decltype(O_)::value;
 #pragma unroll
-    for (int p = 0; p < P; ++p)
+      for (int p = 0; p < P; ++p)
 #pragma unroll
-      for (int k = 0; k < D; ++k) {
-        v[p][k].x = 2 * p < nr ? a.in[(r + 2 * p) * D + k] : 0.f;
-        v[p][k].y = 2 * p + 1 < nr ? a.in[(r + 2 * p + 1) * D + k] : 0.f;
-      }
+        for (int k = 0; k < D; ++k) {
+          v[p][R<D, O>(k)].x = 2 * p < nr ? a.in[(r + 2 * p) * D + k] : 0.f;
+          v[p][R<D, O>(k)].y = 2 * p + 1 < nr ? a.in[(r + 2 * p + 1) * D + k] : 0.f;
+        }
+    };
+    if (odd) load_rows(std::true_type{});
+    else load_rows(std::false_type{});
     uint32_t lab = 0;
     if constexpr (MODE == kLoss) lab = load_labels<D, P>(a.y + r, nr, false);
     f2 ld[P];

@@ -151,35 +151,16 @@ __device__ __forceinline__ void wave_dma(float* sm, const float* __restrict__ sr
   }
 }
 
-// A/B (CNF_SGPR_IN_DIRECT): the lane's two rows (2*D contiguous floats, 16-B
-// aligned when D is even) straight from HBM into registers by 16-B loads,
-// no LDS hop; the compiler's vmcnt wait guards the first use.
-template <int D>
-__device__ __forceinline__ void load_pairs_direct(const float* __restrict__ src, f2 (&v)[1][D]) {
-  static_assert((2 * D) % 4 == 0, "direct row loads need 16-B pairs");
-  using v4 = __attribute__((ext_vector_type(4))) float;
-  float f[2 * D];
-#pragma unroll
-  for (int i = 0; i < D / 2; ++i) {
-#ifdef CNF_SGPR_IN_NT
-    const v4 q = __builtin_nontemporal_load(reinterpret_cast<const v4*>(src) + i);
-#else
-    const v4 q = reinterpret_cast<const v4*>(src)[i];
-#endif
-    f[4 * i] = q.x, f[4 * i + 1] = q.y, f[4 * i + 2] = q.z, f[4 * i + 3] = q.w;
-  }
-#pragma unroll
-  for (int k = 0; k < D; ++k) v[0][k] = f2{f[k], f[D + k]};
-}
-
 // the lane's pairs from the LDS tile (one ds_read2_b32 per feature and pair)
-template <int D, int P>
+// (REV: feature k lands in v[p][D-1-k], the row held reversed)
+template <int D, int P, bool REV = false>
 __device__ __forceinline__ void read_pairs(const float* sm, int lane, f2 (&v)[P][D]) {
   const float* b = sm + 2 * P * D * lane;
 #pragma unroll
   for (int p = 0; p < P; ++p)
 #pragma unroll
-    for (int k = 0; k < D; ++k) v[p][k] = f2{b[2 * p * D + k], b[(2 * p + 1) * D + k]};
+    for (int k = 0; k < D; ++k)
+      v[p][REV ? D - 1 - k : k] = f2{b[2 * p * D + k], b[(2 * p + 1) * D + k]};
 }
 
 // read_pairs with the ds_read2_b32 issued as asm straight into the pair
@@ -187,7 +168,7 @@ __device__ __forceinline__ void read_pairs(const float* sm, int lane, f2 (&v)[P]
 // no use of a row can be scheduled above it.  (The compiler merged the plain
 // loads into ds_read_b128 of four features of one row, and regrouping those
 // into pairs cost ~15 v_mov per tile.)
-template <int D>
+template <int D, bool REV = false>
 __device__ __forceinline__ void read_pairs_wait(const float* sm, int lane, f2 (&v)[1][D]) {
   static_assert(2 * D <= 256, "ds_read2_b32 dword offsets are 8-bit");
   typedef __attribute__((address_space(3))) const float lds_f;
@@ -195,7 +176,7 @@ __device__ __forceinline__ void read_pairs_wait(const float* sm, int lane, f2 (&
 #pragma unroll
   for (int k = 0; k < D; ++k)
     asm volatile("ds_read2_b32 %0, %1 offset0:%2 offset1:%3"
-                 : "=v"(v[0][k])
+                 : "=v"(v[0][REV ? D - 1 - k : k])
                  : "v"(base), "i"(k), "i"(D + k)
                  : "memory");
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");

@@ -1024,7 +1024,9 @@ __global__ __launch_bounds__(256) void k_wbwd_update(
 // ---- the inverse transform's reverse mode (wvjp_inv_run) ----
 
 // z natural -> stash layout of the first inverse step's gathered input
-// z'[j] = z[iq[j]] (flip and rev_perm undone, flows/flows.py:115-117)
+// z'[j] = z[iq[j]] (flip and rev_perm undone, flows/flows.py:115-117).
+// strict: the C part is the reference's whole x_b = mask * z' (0 * z'_T at the
+// mask's zero columns: NaN where z'_T is not finite), raw z'_T in the T part.
 __global__ __launch_bounds__(256) void k_winv_stash(const float* __restrict__ z,
                                                     const int32_t* __restrict__ iqg,
                                                     float* __restrict__ xs, int64_t B, Geo g) {
@@ -1033,14 +1035,21 @@ __global__ __launch_bounds__(256) void k_winv_stash(const float* __restrict__ z,
   const int lane = threadIdx.x & 63;
   const int64_t nw = (int64_t)gridDim.x * 4;
   for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < B; r += nw) {
-    for (int j = lane; j < g.D; j += 64) xs[r * g.Dp + g.col(j)] = z[r * g.D + iq[j]];
-    for (int c = g.DC + lane; c < g.Cp; c += 64) xs[r * g.Dp + c] = c == g.DC ? 1.f : 0.f;
+    for (int j = lane; j < g.D; j += 64) {
+      const float v = z[r * g.D + iq[j]];
+      xs[r * g.Dp + g.col(j)] = v;
+      if (g.strict && j < g.DT) xs[r * g.Dp + j] = 0.f * v;
+    }
+    for (int c = g.ones() + lane; c < g.Cp; c += 64) xs[r * g.Dp + c] = c == g.ones() ? 1.f : 0.f;
     for (int c = g.Cp + g.DT + lane; c < g.Dp; c += 64) xs[r * g.Dp + c] = 0.f;
   }
 }
 
 // One inverse step (flows/flows.py:118-126): x_T = (z'_T - t) e^{-s}, x_C = z'_C;
 // written straight into the next step's gathered stash slot (x[iq_next[j]]).
+// strict: the reference's own op sequence over every feature (b_1 = 1 - mask),
+//   x = x_b + (b_1 (z' - t)) e^{-s},  one rounding per op, so 0 * inf = NaN
+// at masked positions as in torch; the next slot's C part gets x_b again.
 __global__ __launch_bounds__(256) void k_winv_fwd_update(const float* __restrict__ X,
                                                          float* __restrict__ Xn,
                                                          const float* __restrict__ Os,
@@ -1057,46 +1066,69 @@ __global__ __launch_bounds__(256) void k_winv_fwd_update(const float* __restrict
     for (int j = lane; j < g.D; j += 64) {
       const int i = iqn[j];  // next step's z'[j] = this step's x[i]
       float v = xr[g.col(i)];
-      if (i < g.DT) {
-        const float s = Os ? Os[r * g.DTp + i] : 0.f;
-        const float t = Ot ? Ot[r * g.DTp + i] : 0.f;
-        v = __fmul_rn(__fsub_rn(v, t), expf(-s));
+      if (g.strict) {
+        const float b1 = i < g.DT ? 1.f : 0.f;
+        const float sv = Os ? Os[r * g.Op + i] : 0.f;
+        const float tv = Ot ? Ot[r * g.Op + i] : 0.f;
+        const float c = __fmul_rn(b1, __fsub_rn(v, tv));
+        v = __fadd_rn(__fmul_rn(1.f - b1, v), __fmul_rn(c, expf(-sv)));
+        if (j < g.DT) zr[j] = 0.f * v;  // the next step's x_b (mask 0 here)
+      } else if (i < g.DT) {
+        const float sv = Os ? Os[r * g.Op + i] : 0.f;
+        const float tv = Ot ? Ot[r * g.Op + i] : 0.f;
+        v = __fmul_rn(__fsub_rn(v, tv), expf(-sv));
       }
       zr[g.col(j)] = v;
     }
-    for (int c = g.DC + lane; c < g.Cp; c += 64) zr[c] = c == g.DC ? 1.f : 0.f;
+    for (int c = g.ones() + lane; c < g.Cp; c += 64) zr[c] = c == g.ones() ? 1.f : 0.f;
     for (int c = g.Cp + g.DT + lane; c < g.Dp; c += 64) zr[c] = 0.f;
   }
 }
 
 // Back through one inverse step's coupling: g (natural, this step's output) ->
 // tmp (gathered order z'), G_s / G_t for the conditioners.
+// strict: torch autograd's rules for the op sequence of k_winv_fwd_update
+// (c = b_1 (z' - t), x = x_b + c e, e = e^{-s}, ld -= sum b_1 s):
+//   g_c = g e,  G_s = -((g c) e) - gld b_1,  G_t = -(g_c b_1),
+//   g_{z'} = g_c b_1 + mask g   (the conditioners' share, mask-weighted, is
+//   added by the first Linear's back-prop: kEpiAdd with zlt = DT).
 __global__ __launch_bounds__(256) void k_winv_bwd_update(
     const float* __restrict__ gout, float* __restrict__ tmp, const float* __restrict__ X,
     const float* __restrict__ Os, const float* __restrict__ Ot, const float* __restrict__ gld,
     float* __restrict__ Gs, float* __restrict__ Gt, int64_t B, Geo g) {
   const int lane = threadIdx.x & 63;
   const int64_t nw = (int64_t)gridDim.x * 4;
-  const int D = g.D, DT = g.DT, DTp = g.DTp;
+  const int D = g.D, DT = g.DT, Op = g.Op;
   for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < B; r += nw) {
     const float gl = gld[r];
     for (int j = lane; j < D; j += 64) {
       const float v = gout[r * D + j];
       float gz = v;
-      if (j < DT) {
-        const float s = Os ? Os[r * DTp + j] : 0.f;
-        const float t = Ot ? Ot[r * DTp + j] : 0.f;
+      if (g.strict) {
+        const float b1 = j < DT ? 1.f : 0.f;
+        const float s = Os ? Os[r * Op + j] : 0.f;
+        const float t = Ot ? Ot[r * Op + j] : 0.f;
+        const float e = expf(-s);
+        const float c = __fmul_rn(b1, __fsub_rn(X[r * g.Dp + g.col(j)], t));
+        const float gc = __fmul_rn(v, e);
+        const float ga = __fmul_rn(gc, b1);
+        if (Gs) Gs[r * Op + j] = __fsub_rn(-__fmul_rn(__fmul_rn(v, c), e), __fmul_rn(gl, b1));
+        if (Gt) Gt[r * Op + j] = -ga;
+        gz = __fadd_rn(ga, __fmul_rn(1.f - b1, v));
+      } else if (j < DT) {
+        const float s = Os ? Os[r * Op + j] : 0.f;
+        const float t = Ot ? Ot[r * Op + j] : 0.f;
         const float e = expf(-s);
         const float xT = __fmul_rn(__fsub_rn(X[r * g.Dp + g.Cp + j], t), e);
         gz = __fmul_rn(v, e);
-        if (Gs) Gs[r * DTp + j] = __fsub_rn(-__fmul_rn(v, xT), gl);
-        if (Gt) Gt[r * DTp + j] = -gz;
+        if (Gs) Gs[r * Op + j] = __fsub_rn(-__fmul_rn(v, xT), gl);
+        if (Gt) Gt[r * Op + j] = -gz;
       }
       tmp[r * D + j] = gz;
     }
-    for (int i = DT + lane; i < DTp; i += 64) {
-      if (Gs) Gs[r * DTp + i] = 0.f;
-      if (Gt) Gt[r * DTp + i] = 0.f;
+    for (int i = (g.strict ? D : DT) + lane; i < Op; i += 64) {
+      if (Gs) Gs[r * Op + i] = 0.f;
+      if (Gt) Gt[r * Op + i] = 0.f;
     }
   }
 }
@@ -1428,7 +1460,7 @@ int wvjp_workspace(const Shape& s, int64_t B, size_t* bytes) {
 
 // the inverse transform's reverse mode always runs layer at a time
 int wvjp_inv_workspace(const Shape& s, int64_t B, size_t* bytes) {
-  if (!wvjp_ok(s) || s.strict) return CNF_ERR_UNSUPPORTED;
+  if (!wvjp_ok(s)) return CNF_ERR_UNSUPPORTED;
   *bytes = (size_t)make_plan(s, B).total * 4;
   return CNF_OK;
 }
@@ -1686,10 +1718,13 @@ int wvjp_run(const Shape& s, const void* prepared, const float* x, const int64_t
 //   g_{z'_T} = g_T e^{-s},  G_t = -g_T e^{-s},  G_s = -g_T x_T - gld,
 //   g_{z'_C} = g_C + (conditioners' share), then g_{z_in}[iq_l[j]] = g_{z'}[j]
 //   plus the caller's gradient of the previous step's output.
+// strict_nan: every feature follows the reference's op sequence (the strict
+// branches of k_winv_stash / k_winv_fwd_update / k_winv_bwd_update), the nets
+// see all D columns of x_b and write s, t for all D (lin_in / lin_out).
 int wvjp_inv_run(const Shape& s, const void* prepared, const float* z, const float* gx,
                  const float* gx_all, const float* gld_in, float* grads, float* dz, int64_t B,
                  void* ws, size_t ws_bytes, hipStream_t st) {
-  if (!wvjp_ok(s) || s.strict) return CNF_ERR_UNSUPPORTED;  // strict: forward reverse mode only
+  if (!wvjp_ok(s)) return CNF_ERR_UNSUPPORTED;
   // (the workspace is wvjp_inv_workspace's: the layer-at-a-time plan)
   const Plan p = make_plan(s, B);
   if (!ws || ws_bytes < (size_t)p.total * 4) return CNF_ERR_NULL;

@@ -132,10 +132,7 @@ class Flow(nn.Module):
         stack = self._native_stack()
         try:
             if torch.is_grad_enabled() and (x.requires_grad or stack.requires_grad()):
-                if inverse:  # cnf_vjp_inverse
-                    if stack.strict_nan:
-                        _not_native("autograd through the strict-NaN inverse")
-                        return None
+                if inverse:  # cnf_vjp_inverse (strict_nan included)
                     out, ld = stack.inverse_autograd(x, want_all=want_all)
                 else:
                     out, ld = stack.forward_autograd(x, want_all=want_all)
@@ -267,10 +264,7 @@ class NvpCouplingLayer(nn.Module):
             self._stack = CouplingStack([self], strict_nan=strict)
         try:
             if _needs_grad(x, self):
-                if inverse:  # cnf_vjp_inverse
-                    if strict:
-                        _not_native("autograd through the strict-NaN inverse")
-                        return None
+                if inverse:  # cnf_vjp_inverse (strict_nan included)
                     z, ld = self._stack.inverse_autograd(x, want_all=False)
                 else:
                     z, ld = self._stack.forward_autograd(x, want_all=False)

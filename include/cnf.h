@@ -185,7 +185,8 @@ int cnf_loss_vjp(const cnf_desc* desc, const void* prepared, const float* x,
  *   gx     [B][D]     gradient of the final output (xs[-1], the input estimate)
  *   gx_all [L][B][D]  gradient of every step's output (the xs list, step order)
  *   gld    [B]        gradient of the inverse's per-sample log-det
- * Layer-at-a-time MFMA reverse mode for every shape (non-strict). */
+ * Layer-at-a-time MFMA reverse mode for every shape; strict_nan follows
+ * torch autograd's rules for the reference's op sequence (NaN / inf kept). */
 int cnf_vjp_inverse_workspace_bytes(const cnf_desc* desc, int64_t B, size_t* bytes);
 int cnf_vjp_inverse(const cnf_desc* desc, const void* prepared, const float* z, const float* gx,
                     const float* gx_all, const float* gld, float* grads, float* dz, int64_t B,
@@ -214,6 +215,15 @@ int cnf_adam_step(const cnf_desc* desc, float* const* params, const float* grads
 int cnf_adam_step_sched(const cnf_desc* desc, float* const* params, const float* grads,
                         float* exp_avg, float* exp_avg_sq, const float* sched, double beta1,
                         double beta2, double eps, double weight_decay, void* stream);
+
+/* Device-side non-finite guard (failure detection; the counterpart of the
+ * reference's NaN abort, run_experiment3D.py:129-131, without a host sync):
+ * scans n floats of a DEVICE array (z, logdet, loss_terms, gradients ...) and
+ * ORs into the caller-owned DEVICE int32 *flag:  1 if any element is NaN,
+ * 2 if any is +-inf.  The flag is never cleared by the library, so one
+ * zeroed flag can accumulate over many launches and be read once.  One
+ * HBM-bound pass; an atomic OR only from a wave that found something. */
+int cnf_guard_nonfinite(const float* data, int64_t n, int32_t* flag, void* stream);
 
 /* Which kernel family serves this descriptor's launches: "sgpr-fused"
  * (pipelined scalar weights, every output mode), "valu-fused" (strict_nan,

@@ -161,3 +161,19 @@ def test_wide_training_workspace_plans():
     # a ragged batch: the wave-tiled arrays hold whole 32-row blocks
     st, ragged = _vjp_bytes(_lib.make_desc(100, L, [100, 100]), B + 1)
     assert st == 0 and ragged > L * (B + 32) * (640 + 576) * 4
+
+
+def test_guard_argument_validation_without_gpu():
+    """cnf_guard_nonfinite rejects bad arguments before any launch."""
+    import ctypes
+    lib = _lib.lib()
+    P = ctypes.c_void_p
+    flag = ctypes.c_int32(0)
+    buf = (ctypes.c_float * 8)()
+    assert lib.cnf_guard_nonfinite(P(ctypes.addressof(buf)), ctypes.c_int64(-1),
+                                   P(ctypes.addressof(flag)), P(0)) == -4
+    assert lib.cnf_guard_nonfinite(P(ctypes.addressof(buf)), ctypes.c_int64(8), P(0), P(0)) == -1
+    assert lib.cnf_guard_nonfinite(P(0), ctypes.c_int64(8), P(ctypes.addressof(flag)), P(0)) == -1
+    assert lib.cnf_guard_nonfinite(P(ctypes.addressof(buf) + 2), ctypes.c_int64(4),
+                                   P(ctypes.addressof(flag)), P(0)) == -6
+    assert lib.cnf_guard_nonfinite(P(0), ctypes.c_int64(0), P(ctypes.addressof(flag)), P(0)) == 0

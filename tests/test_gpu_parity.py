@@ -77,20 +77,63 @@ def test_inverse_matches_reference_fixture(name):
     got = torch.stack(xs).cpu().numpy()
     if d["inv_xs"].shape[0] == 1:
         got = got[-1:]
-    tol = max(TOL, 2 * _fp32_floor(meta, state, d))
-    assert rel_err(got, d["inv_xs"]) <= tol
-    assert rel_err(ld.cpu().numpy(), d["inv_ld"]) <= tol
+    _check_inverse(name, "every-layer", got, d["inv_xs"], ld.cpu().numpy(), d["inv_ld"],
+                   meta, state, d)
 
 
-def _fp32_floor(meta, state, d):
-    """The reference's own fp32-vs-fp64 error on this inverse (numpy oracle in
-    fp64).  Ill-conditioned cases (exp(-s) up to e^7, g6_d10_h0) sit at ~1e-5
-    by themselves; the bar is then twice the reference's own error."""
+def _inverse64(meta, state, d):
+    """The exact (fp64 numpy oracle) inverse of the fixture's z: every step's x."""
     ly = O.cast_layers(O.layers_from_state(state, meta["L"], meta["D"],
                                            len(meta["hidden"]) + 1, meta["scale"],
                                            meta["shift"]), np.float64)
     xs64, _ = O.flow_inverse(ly, d["zs"][-1].astype(np.float64))
-    return rel_err(d["inv_xs"][-1], xs64[-1])
+    return xs64
+
+
+def _fp32_floor(meta, state, d):
+    """The reference's own fp32-vs-fp64 error on this inverse."""
+    return rel_err(d["inv_xs"][-1], _inverse64(meta, state, d)[-1])
+
+
+def _oracle32_err(meta, state, d):
+    """The numpy oracle's own fp32 inverse against the fixture (the CPU
+    restatement's error on the same case)."""
+    ly = O.layers_from_state(state, meta["L"], meta["D"], len(meta["hidden"]) + 1,
+                             meta["scale"], meta["shift"])
+    xs32, _ = O.flow_inverse(ly, d["zs"][-1].astype(np.float32))
+    return rel_err(np.asarray(xs32[-1], dtype=np.float32), d["inv_xs"][-1])
+
+
+# Fixtures whose inverse is ill-conditioned in fp32 (exp(-s) up to e^7): the
+# reference's own fp32 result sits this far from its fp64 value, so the GPU is
+# held to twice that instead of the flat 1e-5 (DESIGN.md section 5 lists the
+# measured numbers).  Every other fixture is held to 1e-5.
+RELAXED_INVERSE = {"g6_d10_h0"}
+
+
+def _check_inverse(name, path, got_x, ref_x, got_ld, ref_ld, meta, state, d):
+    """Record the GPU inverse error beside the reference's fp32-vs-fp64 error
+    and the oracle's fp32 error (conftest RECORDS -> inverse_errors.jsonl),
+    then hold it to 1e-5, or to 2x the reference's own error for the fixtures
+    in RELAXED_INVERSE."""
+    import conftest
+    e_x, e_ld = rel_err(got_x, ref_x), rel_err(got_ld, ref_ld)
+    x64 = _inverse64(meta, state, d)[-1]
+    floor = rel_err(d["inv_xs"][-1], x64)
+    final = np.asarray(got_x)[-1] if np.asarray(got_x).ndim == 3 else np.asarray(got_x)
+    gpu64 = rel_err(final, x64)
+    conftest.RECORDS.setdefault("inverse_errors", []).append(
+        {"fixture": name, "path": path, "gpu_err_x": e_x, "gpu_err_ld": e_ld,
+         "ref_fp32_vs_fp64": floor, "gpu_vs_fp64": gpu64,
+         "oracle_fp32_err": _oracle32_err(meta, state, d)})
+    if name in RELAXED_INVERSE:
+        # held to twice the reference's own error, against the fixture AND
+        # against the exact answer
+        assert e_x <= max(TOL, 2 * floor) and gpu64 <= max(TOL, 2 * floor), (name, path, e_x,
+                                                                             gpu64, floor)
+    else:
+        assert e_x <= TOL, (name, path, e_x, floor)
+    assert e_ld <= TOL if name not in RELAXED_INVERSE else e_ld <= max(TOL, 2 * floor)
 
 
 def test_fast_mode_on_overflow_case_differs_only_at_reference_nans():
@@ -294,10 +337,9 @@ def test_final_only_inverse_matches_reference_fixture(name):
     with torch.no_grad():
         x, ld = flow.inverse_transform(z)
     assert engine.stats["inverse"] == n0 + 1, "native cnf_inverse did not run"
-    tol = max(TOL, 2 * _fp32_floor(meta, state, d))
-    assert rel_err(x.cpu().numpy(), d["inv_xs"][-1]) <= tol
     assert tuple(ld.shape) == d["inv_ld"].shape
-    assert rel_err(ld.cpu().numpy(), d["inv_ld"]) <= tol
+    _check_inverse(name, "final-only", x.cpu().numpy(), d["inv_xs"][-1], ld.cpu().numpy(),
+                   d["inv_ld"], meta, state, d)
 
 
 @pytest.mark.parametrize("name", [n for n in CASES if n not in ("g6_d4_nan",)])
@@ -322,8 +364,8 @@ def test_valu_family_matches_reference_fixture(name):
     if "inv_xs" in d:
         with torch.no_grad():
             xr, ild = flow.inverse_transform(torch.from_numpy(d["zs"][-1]).to(DEV))
-        tol = max(TOL, 2 * _fp32_floor(meta, state, d))
-        assert rel_err(xr.cpu().numpy(), d["inv_xs"][-1]) <= tol
+        _check_inverse(name, "valu", xr.cpu().numpy(), d["inv_xs"][-1], ild.cpu().numpy(),
+                       d["inv_ld"], meta, state, d)
 
 
 def test_every_layer_outputs_at_full_size():

@@ -112,13 +112,80 @@ def test_strict_fused_loss_vjp_matches_cpu_autograd(kind):
     _same(terms[0] / B, ref_out, "loss")
 
 
-def test_strict_inverse_vjp_stays_unsupported():
-    """Autograd through the strict INVERSE keeps the torch fallback (the ABI
-    reports it unsupported rather than computing non-strict gradients)."""
-    meta, state, _, _ = _case("fixture")
+def _inv_case(kind):
+    """(flow state, z) for the strict INVERSE: the g6_d4_nan stack on a
+    random logit batch, or a variant where exp(-s) overflows at a masked
+    feature in some rows only (s = -200 (w . h) - 88 there), so that
+    b_1 (z - t) e^{-s} = 0 * inf = NaN in those rows (flows/flows.py:123)."""
+    meta, state, d = load("g6_d4_nan")
+    z = torch.from_numpy(d["x"])
+    if kind == "neg_rows":
+        state = dict(state)
+        b = np.array(state["layers.0.s.layers.1.bias"], copy=True)
+        w = np.array(state["layers.0.s.layers.1.weight"], copy=True)
+        b[-1] = -88.0
+        w[-1] *= -200.0
+        state["layers.0.s.layers.1.bias"] = b
+        state["layers.0.s.layers.1.weight"] = w
+        z = z * 8.0
+    return meta, state, z
+
+
+def _inv_xs_objective(f, z):
+    # gradient through every step's output (the xs list) and the log-det
+    xs, ld = f.backward(z)
+    w = torch.arange(1, z.shape[1] + 1, dtype=z.dtype, device=z.device)
+    return sum(((x * w).sum() for x in xs), torch.zeros((), device=z.device)) + 0.5 * ld.sum()
+
+
+def _inv_final_objective(f, z):
+    x, ld = f.inverse_transform(z)
+    w = torch.arange(1, z.shape[1] + 1, dtype=z.dtype, device=z.device)
+    return (x * w).sum() - 0.25 * ld.sum()
+
+
+@pytest.mark.parametrize("kind", ["fixture", "neg_rows"])
+@pytest.mark.parametrize("objective", ["xs", "final"])
+@pytest.mark.parametrize("via_ops", [True, False])
+def test_strict_inverse_vjp_matches_cpu_autograd(kind, objective, via_ops, monkeypatch):
+    """Autograd through the strict INVERSE (Flow.backward, flows/flows.py:
+    114-126) runs cnf_vjp_inverse natively -- through cnf::inverse_flow and
+    through ctypes -- and matches CPU autograd of the reference's own ops,
+    NaN / inf positions included."""
+    monkeypatch.setattr(engine, "USE_TORCH_OPS", via_ops)
+    meta, state, z = _inv_case(kind)
+    obj = _inv_xs_objective if objective == "xs" else _inv_final_objective
+    f_cpu = build_flow(meta, state, "cpu", strict_nan=True)
+    zc = z.clone().requires_grad_(True)
+    ref_out = obj(f_cpu, zc)
+    ps_cpu = [p for p in f_cpu.parameters() if p.requires_grad]
+    ref = torch.autograd.grad(ref_out, ps_cpu + [zc], allow_unused=True)
+    ref = [torch.zeros_like(p) if g is None else g for g, p in zip(ref, ps_cpu + [zc])]
+    f = build_flow(meta, state, DEV, strict_nan=True)
+    assert f._native_stack().has_native_vjp_inverse(), "strict stacks: native inverse reverse mode"
+    zz = z.to(DEV).requires_grad_(True)
+    n0, i0 = engine.stats["vjp"], engine.stats["inverse"]
+    out = obj(f, zz)
+    ps = [p for p in f.parameters() if p.requires_grad]
+    got = torch.autograd.grad(out, ps + [zz], allow_unused=True)
+    torch.cuda.synchronize()
+    assert engine.stats["inverse"] > i0, "native cnf_inverse did not run"
+    if not via_ops:
+        assert engine.stats["vjp"] > n0, "native cnf_vjp_inverse did not run"
+    if kind == "neg_rows":  # the case must really mix NaN and finite rows
+        assert torch.isnan(ref[-1]).any(1).any() and not torch.isnan(ref[-1]).any(1).all()
+    _same(out, ref_out.detach(), "objective")
+    for k, (g, r) in enumerate(zip(got, ref)):
+        _same(torch.zeros_like(r) if g is None else g, r, "grad %d" % k)
+
+
+def test_strict_inverse_workspace_is_reported():
+    """The ABI serves the strict inverse's reverse mode (it reported
+    CNF_ERR_UNSUPPORTED before round 5)."""
+    meta, state, _ = _inv_case("fixture")
     f = build_flow(meta, state, DEV, strict_nan=True)
     import ctypes
     n = ctypes.c_size_t()
     st = _lib.lib().cnf_vjp_inverse_workspace_bytes(ctypes.byref(f._native_stack().desc),
                                                     ctypes.c_int64(4), ctypes.byref(n))
-    assert st == -3
+    assert st == 0 and n.value > 0

@@ -17,6 +17,7 @@
 #   abbits       tools/ab/ab_bits.py (output fingerprints) for the shipped lib and every tools/ab/lib*.so
 #   abtrace      tools/sgpr_trace.py for every tools/ab/lib*.so (trace builds) at AB_TRACE_B rows
 #   abpower      tools/power_probe.py (board power, energy per row) for the shipped lib and every tools/ab/lib*.so
+#   abil         tools/ab/ab_interleave.py: every tools/ab/lib*.so and the shipped lib, interleaved in one process
 #   abterms      tools/ab/ab_terms.py (loss-term bits + fp64 check) for every tools/ab/lib*.so
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -33,7 +34,7 @@ run() {
 }
 for step in "$@"; do
   case "$step" in
-    tests) TAILN=12 run tests 600 python -u -m pytest tests -m gpu -q -rfs --timeout 120 --timeout-method thread ;;
+    tests) TAILN=12 CNF_RECORD_DIR=gpurun_out run tests 600 python -u -m pytest tests -m gpu -q -rfs --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) TAILN=2 run bench 600 python bench.py ;;
     trace) CNF_TRACE_DUMP=gpurun_out/trace_loss.npz run trace_loss 180 python tools/sgpr_trace.py loss && CNF_TRACE_DUMP=gpurun_out/trace_fwd.npz run trace_fwd 180 python tools/sgpr_trace.py forward ;;
@@ -71,6 +72,7 @@ for step in "$@"; do
         n=$(basename "$lib" .so)
         TAILN=1 CNF_HIP_LIB=$PWD/$lib run "power_$n" 120 python tools/power_probe.py ${AB_MODE:-loss} 3 ${AB_B:-1048576}
       done ;;
+    abil) TAILN=${AB_TAIL:-6} run abil 600 python tools/ab/ab_interleave.py ${AB_MODES:-loss,forward} ${AB_BS:-1048576,8388608} ${AB_ROUNDS:-9} ;;
     abterms)
       for lib in tools/ab/lib*.so; do
         [ -e "$lib" ] || continue

@@ -103,6 +103,18 @@ out["per_xcc_start_us_median"] = {int(x): round(float(np.median(start[xcc == x])
 blk = gw // 4
 dec = np.minimum((blk * 10) // max(1, blk.max() + 1), 9)
 out["start_us_by_block_decile"] = [round(float(np.median(start[dec == d])), 2) for d in range(10)]
+# wave start / first data / end by the block's dispatch slot on its CU (0 =
+# the CU's first block): how late the dispatcher places each resident block
+blk_of = gw // 4
+slot = np.zeros(nw, dtype=np.int64)
+for k in np.unique(cu_key):
+    bs = np.unique(blk_of[cu_key == k])
+    for rnk, bb in enumerate(bs):
+        slot[blk_of == bb] = rnk
+out["by_cu_slot"] = {int(r): {"start": round(float(np.median(start[slot == r])), 2),
+                             "data": round(float(np.median(us(a[slot == r, 1]))), 2),
+                             "end": round(float(np.median(end[slot == r])), 2)}
+                     for r in np.unique(slot)}
 print(json.dumps(out))
 if os.environ.get("CNF_TRACE_DUMP"):  # raw marks for offline analysis
     np.savez_compressed(os.environ["CNF_TRACE_DUMP"], marks=raw, clk=clk, B=B)
