@@ -536,6 +536,14 @@ def main():
 
     # dominant kernel: average device time per launch, no collective in between
     k_avg = kernel_only_seconds(runner, max(50, args.steps // 2))
+    # each rank's own kernel-only time beside its step time: on N > 1 the
+    # difference is the NLL all-reduce, the spread across ranks is kernel spread
+    rank_kernel_us = [round(k_avg * 1e6, 3)]
+    if world > 1:
+        kt = torch.tensor([k_avg], dtype=torch.float64, device=dev)
+        every_k = [torch.zeros_like(kt) for _ in range(world)]
+        dist.all_gather(every_k, kt)
+        rank_kernel_us = [round(v.item() * 1e6, 3) for v in every_k]
     bytes_vec = algo_bytes_per_vec(w["D"], w["L"], labels=(mode == "loss"))
     flops_vec = algo_flops_per_vec(w["D"], w["L"], w["hidden"], w["scale"])
     mfma_bound = w["D"] >= 32
@@ -595,6 +603,8 @@ def main():
             # ms/step (ms_per_step above is their max)
             "ranks": dist.get_world_size() if dist.is_initialized() else 1,
             "rank_ms_per_step": rank_ms,
+            # each rank's kernel-only time per launch (no collective in between)
+            "rank_kernel_us": rank_kernel_us,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f32", "data": "synthetic",
             "config": {"workload": "%s: %d-layer %s coupling, D=%d, hidden_size=%s, %d vectors "

@@ -89,7 +89,10 @@ namespace {
 
 using namespace valu;
 
-constexpr int kWaves = 4;  // waves per block
+#ifndef CNF_SGPR_KWAVES  // A/B: waves per block (the grid cap below stays in waves per SIMD)
+#define CNF_SGPR_KWAVES 4
+#endif
+constexpr int kWaves = CNF_SGPR_KWAVES;  // waves per block
 
 // Output path of the full tiles (cnf_sgpr_common.h stage_pairs / store_tile):
 //   0  16-B stores straight from registers, deferred one tile (round 2);
@@ -566,6 +569,9 @@ __global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) v
     }
   };
 
+#ifdef CNF_AB_EMPTY  // A/B timing only: every wave exits at once (launch + drain floor)
+  if (a.B > 0) return;
+#endif
 #ifdef CNF_AB_VGPR80  // A/B: the forward variant forced to >= 80 VGPRs (dispatch-spread test)
   if constexpr (MODE == kFwd) asm volatile("v_mov_b32 v79, 0" ::: "v79");
 #endif
@@ -809,7 +815,7 @@ int resident_blocks(const KV& k, size_t lds) {
 #ifndef CNF_SGPR_GRID_WPS
 #define CNF_SGPR_GRID_WPS 6
 #endif
-  if (n > CNF_SGPR_GRID_WPS) n = CNF_SGPR_GRID_WPS;
+  if (n > CNF_SGPR_GRID_WPS * 4 / kWaves) n = CNF_SGPR_GRID_WPS * 4 / kWaves;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
       cus < 1)

@@ -10,6 +10,7 @@ import ctypes
 import glob
 import json
 import os
+import random
 import statistics
 import sys
 
@@ -36,20 +37,29 @@ for mode in modes:
         wl = "cfg5" if mode == "inverse" else "cfg2"
         w = dict(bench.WORKLOADS[wl], B=B)
         r = bench.Runner(w, dev, 1.0e9, mode="loss" if mode == "loss" else "forward")
-        launches = max(8, (40 << 20) // B)
+        launches = max(24, (160 << 20) // B)
         r.settle(0.5)
         times = {k: [] for k in libs}
+        ratios = {k: [] for k in libs}
+        order = list(libs)
+        rng = random.Random(1234 + B)
         for _ in range(rounds):
-            for k, lib in libs.items():
+            rng.shuffle(order)  # a fresh order every round: no build always follows another
+            got = {}
+            for k in order:
+                lib = libs[k]
                 r.lib = lib
                 r.fn = lib.cnf_inverse if w["inverse"] else lib.cnf_forward
-                times[k].append(bench.kernel_only_seconds(r, launches) * 1e6)
+                got[k] = bench.kernel_only_seconds(r, launches) * 1e6
+                times[k].append(got[k])
+            for k in libs:  # paired with the shipped build of the same round
+                ratios[k].append(got[k] / got["shipped"])
         r.lib = libs["shipped"]
         out = {"mode": mode, "B": B, "rounds": rounds, "launches": launches,
                "median_us": {k: round(statistics.median(v), 2) for k, v in times.items()},
                "min_us": {k: round(min(v), 2) for k, v in times.items()}}
-        base = out["median_us"]["shipped"]
-        out["vs_shipped"] = {k: round(v / base, 4) for k, v in out["median_us"].items()}
+        # median over rounds of (build / shipped) timed in the same round
+        out["vs_shipped"] = {k: round(statistics.median(v), 4) for k, v in ratios.items()}
         print(json.dumps(out), flush=True)
         del r
         torch.cuda.empty_cache()
