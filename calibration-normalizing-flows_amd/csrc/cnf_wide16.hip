@@ -36,6 +36,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 #include <utility>
 
 #include "cnf_internal.h"
@@ -106,6 +107,11 @@ __host__ __device__ constexpr int pad_fwd(int ls) {
   return CNF_W16_LDSA ? cdiv(ls, 2 * kAC) * 2 * kAC : pad_ls(ls, CNF_W16_FWD_P16);
 }
 extern __shared__ __attribute__((aligned(16))) float w16_dyn[];
+// the training forward sweep's A stream through LDS as k_wide16's (A/B): its
+// chunk waits (vmcnt(0)) also cover the tape stores issued since the last one
+#ifndef CNF_W16_TRAIN_LDSA
+#define CNF_W16_TRAIN_LDSA 0
+#endif
 
 // Compile-time geometry of one conditioner MLP (H = 0: absent hidden layer).
 template <int D, int H1, int H2>
@@ -663,8 +669,12 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 struct Rows16 {
   __amdgpu_buffer_rsrc_t rs;
   int voff[2];
-  __device__ __forceinline__ Rows16(const float* block, int W, int lane) {
-    rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(block), 0, kRows * W * 4, 0x00020000);
+  // live = false: a wave wholly past the batch (it still runs the block's
+  // stream for the LDS A-stream barriers): every access falls outside the
+  // descriptor (stores dropped, loads read 0)
+  __device__ __forceinline__ Rows16(const float* block, int W, int lane, bool live = true) {
+    rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(block), 0, live ? kRows * W * 4 : 0,
+                                           0x00020000);
 #pragma unroll
     for (int g = 0; g < 2; ++g) voff[g] = (g * 256 + (lane & 15) * 16 + 4 * (lane >> 4)) * 4;
   }
@@ -816,7 +826,7 @@ __device__ __forceinline__ void net_tape(float (&ring)[P], const float* __restri
       lin<G, NETS, POS, 2, 0>(ring, a, an, bias, h2, ep, lane,
                               std::make_integer_sequence<int, G::mt(2)>{});
     }
-    *reinterpret_cast<v4i*>(bits + 4 * N) = v4i{(int)mb[0], (int)mb[1], (int)mb[2], (int)mb[3]};
+    if (bits) *reinterpret_cast<v4i*>(bits + 4 * N) = v4i{(int)mb[0], (int)mb[1], (int)mb[2], (int)mb[3]};
   }
 }
 
@@ -897,7 +907,8 @@ __global__ __launch_bounds__(64 * kWaves, 2) void k_wtrain16_fwd(
     const float* __restrict__ W, const int32_t* __restrict__ qtab, const float* __restrict__ in,
     float* __restrict__ zst, float* __restrict__ ld_out, float* __restrict__ tape,
     uint32_t* __restrict__ tbits, int64_t B, int L, int Cp, int Dp, SeedArgs sa) {
-  using G = G16<D, H1, H2>;
+  using G = std::conditional_t<CNF_W16_TRAIN_LDSA != 0 && kRunRows == kRows, G16L<D, H1, H2>,
+                               G16<D, H1, H2>>;
   using TP = Tape16<D, H1, H2, NETS>;
   constexpr int XT = G::XT, CT = G::CT, TT = G::TT;
   constexpr int S = D | 1;
@@ -908,8 +919,11 @@ __global__ __launch_bounds__(64 * kWaves, 2) void k_wtrain16_fwd(
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // SGPR: row0, descriptors
   const int64_t row0 = ((int64_t)blockIdx.x * kWaves + wave) * kRows;
-  if (row0 >= B) return;
-  const int nrows = (int)((B - row0) < kRows ? (B - row0) : kRows);
+  // (LDS A stream: the whole block meets every chunk barrier; a wave past the
+  // batch runs the stream on zero rows with its tape descriptors empty)
+  if (!G::kLdsA && row0 >= B) return;
+  const bool live = row0 < B;
+  const int nrows = !live ? 0 : (int)((B - row0) < kRows ? (B - row0) : kRows);
   const int64_t nwb = (B + kRows - 1) / kRows;
   float* st = smem + wave * (kRows * S + D);
   int* qs = reinterpret_cast<int*>(st + kRows * S);
@@ -924,17 +938,30 @@ __global__ __launch_bounds__(64 * kWaves, 2) void k_wtrain16_fwd(
   get_state<G>(st, S, nullptr, X, lane);
   wsync();
 
-  constexpr int P = ring16(LSP, CNF_W16_PMAX);
+  constexpr int P = ring16(LSP, G::kLdsA ? CNF_W16_LDSA_PMAX : CNF_W16_PMAX);
   float ring[P];
+  if constexpr (G::kLdsA) {  // chunks 0 and 1 of the first layer, then the ring from LDS
+    float* stage = w16_dyn + G::kStateFloats;
 #pragma unroll
-  for (int j = 0; j < P; ++j) ring[j] = W[kLaneStride * lane + afrag(j)];
+    for (int k = 0; k < 2 * kAC / 16; ++k)
+      __builtin_amdgcn_global_load_lds(const_cast<float*>(W + kLaneStride * lane + 256 * (4 * k + wave)),
+                                       stage + 256 * (4 * k + wave), 16, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < P; ++j) ring[j] = stage[afrag(j) + 4 * lane];
+  } else {
+#pragma unroll
+    for (int j = 0; j < P; ++j) ring[j] = W[kLaneStride * lane + afrag(j)];
+  }
   float ld[2] = {0.f, 0.f};
   for (int l = 0; l < L; ++l) {
     const int ln = l + 1 < L ? l + 1 : l;
     const float* __restrict__ wl = W + (int64_t)l * LF + kLaneStride * lane;
     const float* __restrict__ wn = W + (int64_t)ln * LF + kLaneStride * lane;
     const float* __restrict__ bl = W + (int64_t)l * LF + LA;
-    const Rows16 tp(tape + ((int64_t)l * nwb * kRows + row0) * TP::RW, TP::RW, lane);
+    const Rows16 tp(tape + ((int64_t)l * nwb * kRows + (live ? row0 : 0)) * TP::RW, TP::RW, lane,
+                    live);
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
 #pragma unroll
@@ -951,7 +978,9 @@ __global__ __launch_bounds__(64 * kWaves, 2) void k_wtrain16_fwd(
     v4 Tv[TT][2];
     EpOut<false, TT> et{Tv};
     // this wave's relu' bits: 8 words per lane (4 per net)
-    uint32_t* bp = tbits + ((int64_t)l * nwb + row0 / kRows) * 512 + lane * 8;
+    // (a wave past the batch writes its bits into block 0's record of this
+    // layer ... never: net_tape stores them only when `bp` is non-null)
+    uint32_t* bp = live ? tbits + ((int64_t)l * nwb + row0 / kRows) * 512 + lane * 8 : nullptr;
     if constexpr (NETS == 2) {  // forward stream: t-net (tape net 1), then s-net (net 0)
       net_tape<G, TP, 2, 0, 1>(ring, wl, wn, bl, X, et, tp, bp, lane);
       EpAffineTape<XT, CT, TT, TP::So> ea{X, Tv, ld, tp};
@@ -965,6 +994,10 @@ __global__ __launch_bounds__(64 * kWaves, 2) void k_wtrain16_fwd(
     }
     pad_steps<G, NETS, P>(ring, wl, wn, std::make_integer_sequence<int, LSP - NETS * G::steps()>{});
     relayout<G>(st, qs, S, qtab + l * D, X, lane);
+  }
+  if constexpr (G::kLdsA) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the block
+    if (!live) return;
   }
 
   put_state<G>(st, S, X, lane);
@@ -1476,7 +1509,10 @@ int wide16_train_forward(const Shape& s, const void* prepared, const float* x, f
     sa.grad_scale = seed->grad_scale;
     sa.kind = seed->kind;
   }
-  hipLaunchKernelGGL(e->tfwd[s.nets - 1], grid, block, w16_lds(s), st, W, fwd_q, x, zst, ld, tape,
+  const size_t lds = CNF_W16_TRAIN_LDSA && kRunRows == kRows
+                         ? (size_t)(cdiv(kWaves * (kRows * (s.D | 1) + s.D), 64) * 64 + 2 * kAC * 64) * 4
+                         : w16_lds(s);
+  hipLaunchKernelGGL(e->tfwd[s.nets - 1], grid, block, lds, st, W, fwd_q, x, zst, ld, tape,
                      tbits, B, s.L, Cp, Dp, sa);
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) {

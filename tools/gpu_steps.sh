@@ -18,6 +18,7 @@
 #   abtrace      tools/sgpr_trace.py for every tools/ab/lib*.so (trace builds) at AB_TRACE_B rows
 #   abpower      tools/power_probe.py (board power, energy per row) for the shipped lib and every tools/ab/lib*.so
 #   abil         tools/ab/ab_interleave.py: every tools/ab/lib*.so and the shipped lib, interleaved in one process
+#   abwide       tools/ab/ab_wide_train.py (cfg4 training step) for the shipped lib and every tools/ab/lib*.so, x3
 #   abterms      tools/ab/ab_terms.py (loss-term bits + fp64 check) for every tools/ab/lib*.so
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -73,6 +74,15 @@ for step in "$@"; do
         TAILN=1 CNF_HIP_LIB=$PWD/$lib run "power_$n" 120 python tools/power_probe.py ${AB_MODE:-loss} 3 ${AB_B:-1048576}
       done ;;
     abil) TAILN=${AB_TAIL:-6} run abil 600 python tools/ab/ab_interleave.py ${AB_MODES:-loss,forward} ${AB_BS:-1048576,8388608} ${AB_ROUNDS:-9} ;;
+    abwide)  # cfg4 training step per build, separate processes, shipped / builds interleaved
+      for rep in 1 2 3; do
+        TAILN=1 run abwide_shipped_$rep 300 python tools/ab/ab_wide_train.py
+        for lib in tools/ab/lib*.so; do
+          [ -e "$lib" ] || continue
+          n=$(basename "$lib" .so)
+          TAILN=1 CNF_HIP_LIB=$PWD/$lib run "abwide_${n}_$rep" 300 python tools/ab/ab_wide_train.py
+        done
+      done ;;
     abterms)
       for lib in tools/ab/lib*.so; do
         [ -e "$lib" ] || continue
