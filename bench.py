@@ -281,9 +281,16 @@ def train_step_rate(dev, workload="cfg2", B=None, steps=20):
     flow = make_flow(w, dev)
     stack = flow._native_stack()
     x, y = synthetic_logits(B, w["D"], dev, 4321)
-    for _ in range(3):
-        V.loss_and_grads(stack, x, y, grad_scale=1.0 / B)
-    torch.cuda.synchronize(dev)
+    # untimed steps until the device has run ~0.3 s (the clock ramp, as
+    # Runner.settle): 3 warmup steps timed 0.2007 ms per cfg2 step, the same
+    # step back to back 0.179 ms at 2.39 GHz (tools/power_probe.py train)
+    t0 = time.perf_counter()
+    while True:
+        for _ in range(8):
+            V.loss_and_grads(stack, x, y, grad_scale=1.0 / B)
+        torch.cuda.synchronize(dev)
+        if time.perf_counter() - t0 >= 0.3:
+            break
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(steps):
@@ -581,7 +588,7 @@ def main():
                               "bound": rf["bound"], "frac": rf["frac"]}
             del r
             torch.cuda.empty_cache()
-        variants["cfg2_train_step_fused_loss_vjp"] = train_step_rate(dev)
+        variants["cfg2_train_step_fused_loss_vjp"] = train_step_rate(dev, steps=100)
         variants["cfg4_train_step_loss_vjp"] = train_step_rate(dev, "cfg4", steps=5)
         variants["calibrator_fit_epoch"] = calibrator_epoch_rate(dev)
 

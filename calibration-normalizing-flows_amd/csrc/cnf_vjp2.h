@@ -92,7 +92,10 @@ __device__ __forceinline__ void static_for(F&& f) {
 }
 
 constexpr int kV2TR = 128;   // rows per wave tile (lane l: rows 2l, 2l+1)
-constexpr int kV2LMax = 8;   // layers the register accumulators hold
+#ifndef CNF_V2_LMAX
+#define CNF_V2_LMAX 8
+#endif
+constexpr int kV2LMax = CNF_V2_LMAX;  // layers the register accumulators hold
 constexpr int kV2SS = 68;    // stage row stride in floats (64 rows + pad, 16-B aligned)
 
 
@@ -211,18 +214,37 @@ __device__ __forceinline__ void vnet_fwd_sp(const float* wn, const f2* c, f2* h1
   }
 }
 
-// relu' from the stored activation h, as torch's threshold_backward: drops g
-// where h <= 0 and keeps it otherwise (a NaN activation passes g through)
+// relu' from the recomputed activation h' = 2^-64 relu(pre) (the clamp-ReLU
+// output of vnet_fwd_sp: in [0, 1], 0 for a NaN pre-activation), as torch's
+// threshold_backward: drops g where h' = 0 and keeps it otherwise.
+// Default (2): clamp((h' 2^127) 2^127) * g, three packed ops per pair, no VCC
+// (the compare-and-select form, 0, costs two v_cmp + two v_cndmask per pair
+// plus the VCC hazard's wait states): 0.1765 -> 0.1750 ms per cfg2 step,
+// gradients bitwise unchanged.
 #ifndef CNF_V2_CLAMP_MASK
+#define CNF_V2_CLAMP_MASK 2
+#endif
+#if CNF_V2_CLAMP_MASK == 0
 __device__ __forceinline__ f2 relu_mask(f2 g, f2 h) {
   return f2{h.x <= 0.f ? 0.f : g.x, h.y <= 0.f ? 0.f : g.y};
 }
-#else
+#elif CNF_V2_CLAMP_MASK == 1
 // A/B: the mask as clamp(h' 2^127) (packed; NaN clamps to 0) times g -- exact
 // for h' = 2^-64 h >= 2^-127, i.e. every pre-activation above 2^-63
 __device__ __forceinline__ f2 relu_mask(f2 g, f2 h) {
   f2 m;
   asm("v_pk_mul_f32 %0, %1, %2 clamp" : "=v"(m) : "v"(h), "s"(splat(0x1p127f, f2{})));
+  return g * m;
+}
+#else
+// clamp((h' 2^127) 2^127) times g -- exact for every h' > 0 (f32
+// denormals are kept: the smallest, 2^-149, maps to 2^105 before the clamp);
+// h' is the clamp-ReLU output, so h' in [0, 1] and 0 for a NaN pre-activation
+__device__ __forceinline__ f2 relu_mask(f2 g, f2 h) {
+  f2 m, u;
+  const f2 k = splat(0x1p127f, f2{});
+  asm("v_pk_mul_f32 %0, %1, %2" : "=v"(u) : "v"(h), "s"(k));
+  asm("v_pk_mul_f32 %0, %1, %2 clamp" : "=v"(m) : "v"(u), "s"(k));
   return g * m;
 }
 #endif
@@ -304,6 +326,80 @@ __device__ __forceinline__ floatx4 wgrad_tile(float* st, const f2* G, const f2* 
   return acc;
 }
 
+// CNF_V2_PIPE=1 (A/B; measured 0.1796-0.1805 ms per cfg2 step against
+// 0.1778-0.1791 for the default): the dW stage holds the whole 128-row tile (G features
+// 0..15, H 16..31; lane l's rows at columns l and 64 + l) and is software-
+// pipelined against the VALU: a net's stage is written, then independent VALU
+// work runs (the other net's back-propagation, or the next layer's recompute)
+// while the 62 stores drain, and only then is it folded.  The fold streams its
+// operands with the next float4 pair in flight behind each 4-MFMA group.
+// 0 (default) = the 64-row stage folded right after it is written
+// (wgrad_tile): the block's second wave already covers those LDS waits.
+#ifndef CNF_V2_PIPE
+#define CNF_V2_PIPE 0
+#endif
+#ifndef CNF_V2_HLATE
+#define CNF_V2_HLATE 1  // the dW stack's 2^64 on h' applied once per wave (below)
+#endif
+#ifndef CNF_V2_TLATE
+#define CNF_V2_TLATE 0  // A/B: the t-net recompute after the s-net's backward step
+#endif
+// Stage row stride 136 floats: a lane (i = l%16, q = l/16) reads float4 c of
+// feature i at i*136 + 16c + 4q, so every 16-lane group of ds_read_b128 lands
+// on 64 distinct banks (136/4 = 34 = 2 mod 16 puts the q-odd lanes on the odd
+// 4-bank slots), and 64 consecutive lanes store 64 consecutive floats.
+constexpr int kV2SP = 136;
+#ifndef CNF_V2_WPS
+#define CNF_V2_WPS 2  // waves per SIMD the register budget is held to
+#endif
+
+template <int GS, int HS>
+__device__ __forceinline__ void stage_put(float* st, const f2* G, const f2* H, int lane) {
+#pragma unroll
+  for (int f = 0; f < GS; ++f) {
+    st[f * kV2SP + lane] = G[f].x;
+    st[f * kV2SP + 64 + lane] = G[f].y;
+  }
+#pragma unroll
+  for (int f = 0; f < HS; ++f) {
+    st[(16 + f) * kV2SP + lane] = H[f].x;
+    st[(16 + f) * kV2SP + 64 + lane] = H[f].y;
+  }
+}
+
+// acc += G^T H over the staged 128 rows: 32 MFMA steps, lane (i, q) feeding
+// rows 16c + 4q + e (c < 8, e < 4) of feature i.  The reads are inline asm so
+// that the next float4 pair is issued before the current group's MFMAs; each
+// pair is waited for with a counted lgkmcnt (LDS returns in order; an SMEM
+// load in between only makes the count wait longer) and laundered through an
+// empty asm after the wait, so no MFMA can be scheduled above it.
+__device__ __forceinline__ floatx4 stage_fold(const float* st, int lane, floatx4 acc) {
+  typedef __attribute__((address_space(3))) float lds_f;
+  const uint32_t a = (uint32_t)(uintptr_t)(lds_f*)(st + (lane & 15) * kV2SP + 4 * (lane >> 4));
+  constexpr int kB = 16 * kV2SP * 4;  // byte offset of the H features
+  floatx4 A[2], Bv[2];
+  asm volatile("ds_read_b128 %0, %1" : "=v"(A[0]) : "v"(a) : "memory");
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(Bv[0]) : "v"(a), "i"(kB) : "memory");
+  static_for<0, 8>([&](auto C) __attribute__((always_inline)) {
+    constexpr int c = decltype(C)::value, cur = c & 1, nxt = cur ^ 1;
+    if constexpr (c < 7) {
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(A[nxt]) : "v"(a), "i"(64 * (c + 1))
+                   : "memory");
+      asm volatile("ds_read_b128 %0, %1 offset:%2"
+                   : "=v"(Bv[nxt]) : "v"(a), "i"(kB + 64 * (c + 1)) : "memory");
+      asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    asm volatile("" : "+v"(A[cur]), "+v"(Bv[cur]));
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(A[cur].x, Bv[cur].x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(A[cur].y, Bv[cur].y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(A[cur].z, Bv[cur].z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(A[cur].w, Bv[cur].w, acc, 0, 0, 0);
+  });
+  return acc;
+}
+
 // parameter p (state_dict order of one layer) -> (G row i, H column j) of its
 // gradient in the (layer, net) tile, or -1 when the gradient is zero by the mask
 // (the transformed-half inputs of the first Linear, the conditioning-half
@@ -366,7 +462,7 @@ __device__ __forceinline__ int cell_param(int i, int j) {
 }
 
 template <int D, int H1, int H2, int NETS, bool LOSS, bool PERM>
-__global__ __launch_bounds__(64, 2) void k_vjp2(const float* __restrict__ W,
+__global__ __launch_bounds__(64, CNF_V2_WPS) void k_vjp2(const float* __restrict__ W,
                                                 const int32_t* __restrict__ fq,
                                                 const int32_t* __restrict__ iq,
                                                 const int32_t* __restrict__ lflag, VArgs2 a) {
@@ -378,7 +474,14 @@ __global__ __launch_bounds__(64, 2) void k_vjp2(const float* __restrict__ W,
   constexpr int TF = kV2TR * D;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* tile = smem;        // [TF] input rows
+#if CNF_V2_PIPE
+  // the tile is done with (forward read, seed) before the first stage write
+  float* st = smem;          // [32][kV2SP] G / H stage of all 128 rows
+  constexpr int kStage = 32 * kV2SP;
+#else
   float* st = smem + TF;     // [32][kV2SS] G / H stage
+  constexpr int kStage = 32 * kV2SS;
+#endif
   const int lane = threadIdx.x;
   const int64_t B = a.B;
   const int L = a.L;
@@ -389,12 +492,21 @@ __global__ __launch_bounds__(64, 2) void k_vjp2(const float* __restrict__ W,
   // the plain one (back-propagation): cnf_prepare's sp_region / vp_region
   const float* __restrict__ Wsp = W - (int64_t)L * LF;
   constexpr float kTwo64 = 0x1p64f;  // h = 2^64 h' (exact)
+#if CNF_V2_HLATE
+  // H takes h' itself: the hidden columns of the accumulators are 2^-64 times
+  // the gradient and get the 2^64 once, when the wave writes its partial (a
+  // power-of-two scale commutes with every rounding of the sum until the
+  // products fall below 2^-126, i.e. |g h| < 2^-62)
+  constexpr float kHs = 1.f;
+#else
+  constexpr float kHs = kTwo64;
+#endif
   floatx4 acc[kV2LMax][NETS];
 #pragma unroll
   for (int l = 0; l < kV2LMax; ++l)
 #pragma unroll
     for (int n = 0; n < NETS; ++n) acc[l][n] = floatx4{0.f, 0.f, 0.f, 0.f};
-  for (int i = lane; i < 32 * kV2SS; i += 64) st[i] = 0.f;
+  for (int i = lane; i < kStage; i += 64) st[i] = 0.f;
   float lt0 = 0.f, lt1 = 0.f, lt2 = 0.f;
 
   for (int tix = blockIdx.x; tix < ntiles; tix += gridDim.x) {
@@ -671,7 +783,9 @@ __global__ __launch_bounds__(64, 2) void k_vjp2(const float* __restrict__ W,
       // their sign; the weight-gradient stack H takes 2^64 times them)
       const float* ws = Wsp + lofs;
       f2 th1[H1 ? H1 : 1], th2[H2 ? H2 : 1], t[DT];
+#if !CNF_V2_TLATE
       vnet_fwd_sp<S, NC>(ws + (NETS == 2 ? S::NF : 0), c, th1, th2, t);
+#endif
       f2 H[HS];
 #pragma unroll
       for (int k = 0; k < DC; ++k) H[k] = c[k];
@@ -681,6 +795,13 @@ __global__ __launch_bounds__(64, 2) void k_vjp2(const float* __restrict__ W,
       if constexpr (NETS == 2) {
         f2 sh1[H1 ? H1 : 1], sh2[H2 ? H2 : 1], sv[DT];
         vnet_fwd_sp<S, NC>(ws, c, sh1, sh2, sv);  // sv = log2(e) s
+#if CNF_V2_PIPE
+        // layer l+1's t-net stage, written at the end of its backward step,
+        // drained behind this layer's recompute
+        if constexpr (l + 1 < kV2LMax) {
+          if (l + 1 < L) acc[l + 1][1] = stage_fold(st, lane, acc[l + 1][1]);
+        }
+#endif
         f2 gs[DT];
 #pragma unroll
         for (int j = 0; j < DT; ++j) {
@@ -695,12 +816,25 @@ __global__ __launch_bounds__(64, 2) void k_vjp2(const float* __restrict__ W,
           for (int f = 0; f < GS; ++f) G[f] *= keep;
         }
 #pragma unroll
-        for (int m = 0; m < H1; ++m) H[DC + m] = sh1[m] * splat(kTwo64, f2{});
+        for (int m = 0; m < H1; ++m) H[DC + m] = sh1[m] * splat(kHs, f2{});
 #pragma unroll
-        for (int m = 0; m < H2; ++m) H[DC + H1 + m] = sh2[m] * splat(kTwo64, f2{});
+        for (int m = 0; m < H2; ++m) H[DC + H1 + m] = sh2[m] * splat(kHs, f2{});
+#if CNF_V2_PIPE
+        stage_put<GS, HS>(st, G, H, lane);  // folded after the t-net's VALU below
+#else
         acc[l][0] = wgrad_tile<GS, HS>(st, G, H, lane, acc[l][0]);
+#endif
       }
+#if CNF_V2_PIPE
+      if constexpr (NETS == 1 && l + 1 < kV2LMax) {  // (see the s-net branch)
+        if (l + 1 < L) acc[l + 1][0] = stage_fold(st, lane, acc[l + 1][0]);
+      }
+#endif
       {  // t-net: d/dt = g_T (before the e^s scaling of the s-net branch)
+#if CNF_V2_TLATE
+        // recomputed only now: th1 / th2 are not live across the s-net's step
+        vnet_fwd_sp<S, NC>(ws + (NETS == 2 ? S::NF : 0), c, th1, th2, t);
+#endif
         f2 G[GS];
         f2 gt[DT];
 #pragma unroll
@@ -710,11 +844,18 @@ __global__ __launch_bounds__(64, 2) void k_vjp2(const float* __restrict__ W,
 #pragma unroll
           for (int f = 0; f < GS; ++f) G[f] *= keep;
         }
+#if CNF_V2_PIPE
+        if constexpr (NETS == 2) acc[l][0] = stage_fold(st, lane, acc[l][0]);
+#endif
 #pragma unroll
-        for (int m = 0; m < H1; ++m) H[DC + m] = th1[m] * splat(kTwo64, f2{});
+        for (int m = 0; m < H1; ++m) H[DC + m] = th1[m] * splat(kHs, f2{});
 #pragma unroll
-        for (int m = 0; m < H2; ++m) H[DC + H1 + m] = th2[m] * splat(kTwo64, f2{});
+        for (int m = 0; m < H2; ++m) H[DC + H1 + m] = th2[m] * splat(kHs, f2{});
+#if CNF_V2_PIPE
+        stage_put<GS, HS>(st, G, H, lane);  // folded by layer l - 1 (or after the sweep)
+#else
         acc[l][NETS - 1] = wgrad_tile<GS, HS>(st, G, H, lane, acc[l][NETS - 1]);
+#endif
       }
 #pragma unroll
       for (int j = 0; j < DT; ++j) {
@@ -728,6 +869,9 @@ __global__ __launch_bounds__(64, 2) void k_vjp2(const float* __restrict__ W,
       constexpr int l = kV2LMax - 1 - decltype(I)::value;
       if (l < L) bwd(std::integral_constant<int, l>{});
     });
+#if CNF_V2_PIPE
+    acc[0][NETS - 1] = stage_fold(st, lane, acc[0][NETS - 1]);  // layer 0's t-net
+#endif
     if (a.dx) {
 #pragma unroll
       for (int j = 0; j < D; ++j) {
@@ -742,29 +886,52 @@ __global__ __launch_bounds__(64, 2) void k_vjp2(const float* __restrict__ W,
   const int P = a.P;
   constexpr int NFN = H1 == 0 ? D * D + D : (H2 == 0 ? H1 * D + H1 + D * H1 + D
                                                       : H1 * D + H1 + H2 * H1 + H2 + D * H2 + D);
-  // zeros where the mask makes the gradient vanish
-  for (int p = lane; p < P; p += 64) {
-    int n;
-    const int l = p / (NETS * NFN);
-    if (param_cell<D, H1, H2, NETS>(p - l * NETS * NFN, &n) < 0) out[p] = 0.f;
+  // zeros where the mask makes the gradient vanish: the same offsets in every
+  // (layer, net) block, so the lane classifies its offsets lane + 64 k of one
+  // block once (a param_cell per element of P was ~4 % of the launch's VALU)
+  {
+    constexpr int KB = (NFN + 63) / 64;
+    bool zr[KB];
+#pragma unroll
+    for (int k = 0; k < KB; ++k) {
+      int n;
+      const int rr = lane + 64 * k;
+      zr[k] = rr < NFN && param_cell<D, H1, H2, 1>(rr, &n) < 0;
+    }
+    for (int blk = 0; blk < L * NETS; ++blk)
+#pragma unroll
+      for (int k = 0; k < KB; ++k)
+        if (zr[k]) out[blk * NFN + lane + 64 * k] = 0.f;
   }
   // the lane's accumulator cells: C[i = 4 (lane/16) + e][j = lane % 16]
   const int j = lane & 15, i0 = 4 * (lane >> 4);
-  static_for<0, kV2LMax>([&](auto I) __attribute__((always_inline)) {
-    constexpr int l = decltype(I)::value;
-    if (l >= L) return;
+  const float hsc = (CNF_V2_HLATE && j >= DC && j < DC + H1 + H2) ? kTwo64 : 1.f;
+  // the cells' offsets within a net's block: the same for every (layer, net),
+  // mapped once (laundered, so the mapping is not re-derived per store) and
+  // gathered into one exec mask
+  int q[4];
+  bool any = false;
 #pragma unroll
-    for (int n = 0; n < NETS; ++n) {
-      const floatx4 c4 = acc[l][n];
-      // net n's parameters follow the layer's state_dict order: s-net first
-      const int base = l * NETS * NFN + n * NFN;
+  for (int e = 0; e < 4; ++e) {
+    q[e] = cell_param<D, H1, H2>(i0 + e, j);
+    asm volatile("" : "+v"(q[e]));
+    any |= q[e] >= 0;
+  }
+  if (any) {
+    static_for<0, kV2LMax>([&](auto I) __attribute__((always_inline)) {
+      constexpr int l = decltype(I)::value;
+      if (l >= L) return;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int q = cell_param<D, H1, H2>(i0 + e, j);
-        if (q >= 0) out[base + q] = c4[e];
+      for (int n = 0; n < NETS; ++n) {
+        const floatx4 c4 = acc[l][n];
+        // net n's parameters follow the layer's state_dict order: s-net first
+        float* ob = out + l * NETS * NFN + n * NFN;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (q[e] >= 0) ob[q[e]] = c4[e] * hsc;
       }
-    }
-  });
+    });
+  }
   if constexpr (LOSS) {
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {

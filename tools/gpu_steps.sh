@@ -19,6 +19,7 @@
 #   abpower      tools/power_probe.py (board power, energy per row) for the shipped lib and every tools/ab/lib*.so
 #   abil         tools/ab/ab_interleave.py: every tools/ab/lib*.so and the shipped lib, interleaved in one process
 #   abwide       tools/ab/ab_wide_train.py (cfg4 training step) for the shipped lib and every tools/ab/lib*.so, x3
+#   abvjp        tools/ab/ab_vjp.py (cfg2 training step + gradient checksum) for the shipped lib and every tools/ab/lib*.so, x3
 #   abterms      tools/ab/ab_terms.py (loss-term bits + fp64 check) for every tools/ab/lib*.so
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -81,6 +82,15 @@ for step in "$@"; do
           [ -e "$lib" ] || continue
           n=$(basename "$lib" .so)
           TAILN=1 CNF_HIP_LIB=$PWD/$lib run "abwide_${n}_$rep" 300 python tools/ab/ab_wide_train.py
+        done
+      done ;;
+    abvjp)  # cfg2 training step per build, separate processes, shipped / builds interleaved
+      for rep in 1 2 3; do
+        TAILN=1 run abvjp_shipped_$rep 300 python tools/ab/ab_vjp.py
+        for lib in tools/ab/lib*.so; do
+          [ -e "$lib" ] || continue
+          n=$(basename "$lib" .so)
+          TAILN=1 CNF_HIP_LIB=$PWD/$lib run "abvjp_${n}_$rep" 300 python tools/ab/ab_vjp.py
         done
       done ;;
     abterms)

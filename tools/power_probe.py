@@ -1,7 +1,8 @@
 """Board power and clocks while the cfg2 bench pass runs back to back: is the
 device at its power cap (the shader clock then falls as memory traffic is
 added, tools/sgpr_trace.py clock_ghz)?  Samples `rocm-smi` (read-only) idle
-and under load.  usage: power_probe.py [loss|forward] [seconds]"""
+and under load.  usage: power_probe.py [loss|forward|train] [seconds] [B]
+(train: the fused calibrator step, cnf_loss_vjp + reduction)."""
 import json
 import os
 import subprocess
@@ -30,7 +31,21 @@ def smi():
 
 
 dev = torch.device("cuda:0")
-r = bench.Runner(dict(bench.WORKLOADS["cfg2"], B=B), dev, 1.0e9, mode=mode)
+if mode == "train":
+    from cnf_hip import vjp as V
+
+    class _Train:
+        def __init__(self):
+            w = bench.WORKLOADS["cfg2"]
+            self.stack = bench.make_flow(w, dev)._native_stack()
+            self.x, self.y = bench.synthetic_logits(B, w["D"], dev, 4321)
+
+        def step(self):
+            V.loss_and_grads(self.stack, self.x, self.y, grad_scale=1.0 / B)
+
+    r = _Train()
+else:
+    r = bench.Runner(dict(bench.WORKLOADS["cfg2"], B=B), dev, 1.0e9, mode=mode)
 res = {"lib": os.path.basename(os.environ.get("CNF_HIP_LIB", "libcnf_hip.so")), "mode": mode,
        "B": B, "idle": smi()}
 stop = threading.Event()
@@ -49,7 +64,7 @@ th.start()
 t0 = time.perf_counter()
 t_end = t0 + secs
 n = 0
-per = max(1, (200 << 20) // B)
+per = max(1, ((200 if mode != "train" else 25) << 20) // B)
 while time.perf_counter() < t_end:
     for _ in range(per):
         r.step()
