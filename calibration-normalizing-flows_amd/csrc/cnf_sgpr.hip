@@ -439,8 +439,9 @@ __device__ __forceinline__ void pair_predict(f2* v, const float* __restrict__ lp
 // Launch arguments besides the read-only tables, which travel as separate
 // __restrict__ kernel parameters: a pointer the compiler cannot prove
 // unaliased by the kernel's stores is read with vector loads, not s_load.
+// (the input rows and the batch size are the kernel's leading arguments, so
+// that kernarg preloading puts them in SGPRs before the wave starts: see k_sgpr)
 struct KArgs {
-  const float* in;
   float* out;             // final z / x / probabilities (nullable except predict)
   float* ld;              // per-row log-det (nullable)
   float* all;             // [L][B][D] every-layer outputs (ALL variants)
@@ -448,7 +449,6 @@ struct KArgs {
   float* part;            // per-block loss partials, 4 floats each (loss)
   uint32_t* ctr;          // arrival counter of the in-launch block-order sum (loss)
   float* terms;           // loss_terms[3] (loss, in-launch sum)
-  int64_t B;
   int L, kind;
   float det;
 };
@@ -458,7 +458,15 @@ struct KArgs {
 // every layer's output.  PERM: some layer has a random_flip permutation.
 // A lane carries P row pairs (2P rows), a wave tile 128*P rows.
 template <int D, int H1, int H2, int NETS, int MODE, bool ALL, bool PERM>
+//
+// Argument order: the first three (rows in, batch size, weight region) are
+// what a wave needs to issue its first tile's LDS-DMA and weight loads; the
+// Makefile builds this file with kernarg preloading of them
+// (-amdgpu-kernarg-preload-count), so they arrive in SGPRs with the wave
+// instead of through dependent s_loads of the argument block.
 __global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) void k_sgpr(
+    const float* __restrict__ in,       // rows [B][D]
+    int64_t B,
     const float* __restrict__ W,        // packed-SGPR weight region
     const int32_t* __restrict__ qtab,   // per-layer gather tables (forward or inverse)
     const int32_t* __restrict__ lflag,  // per-layer flags
@@ -474,7 +482,6 @@ __global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) v
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   float* sm = smem + wv * TF;
-  const int64_t B = a.B;
   const int L = a.L;
   const int nfull = (int)(B / TR), ntiles = (int)((B + TR - 1) / TR);
   const int gw = blockIdx.x * kWaves + wv, nw = gridDim.x * kWaves;
@@ -570,7 +577,7 @@ __global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) v
   };
 
 #ifdef CNF_AB_EMPTY  // A/B timing only: every wave exits at once (launch + drain floor)
-  if (a.B > 0) return;
+  if (B > 0) return;
 #endif
 #ifdef CNF_AB_VGPR80  // A/B: the forward variant forced to >= 80 VGPRs (dispatch-spread test)
   if constexpr (MODE == kFwd) asm volatile("v_mov_b32 v79, 0" ::: "v79");
@@ -605,7 +612,7 @@ __global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) v
 #else
   constexpr bool kNoMem = false;
 #endif
-  if (!kNoMem && t < nfull) wave_dma<D, TR>(sm, a.in + (int64_t)t * TF, lane);
+  if (!kNoMem && t < nfull) wave_dma<D, TR>(sm, in + (int64_t)t * TF, lane);
   auto set_prio = [&]() {
     --left;  // tiles after this one
 #ifndef CNF_AB_NO_PRIO
@@ -651,7 +658,7 @@ __global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) v
       }
       if (a.ld) store_lds<P>(a.ld + prow, pld, 2 * P, al_ld);
     }
-    if (kStage != 1 && t + nw < nfull) wave_dma<D, TR>(sm, a.in + (int64_t)(t + nw) * TF, lane);
+    if (kStage != 1 && t + nw < nfull) wave_dma<D, TR>(sm, in + (int64_t)(t + nw) * TF, lane);
     uint32_t lab = 0;
     if constexpr (MODE == kLoss)
       if (!kNoMem) lab = load_labels<D, P>(a.y + row0 + 2 * P * lane, 2 * P, y16);
@@ -680,7 +687,7 @@ __global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) v
       }
       if (a.ld) store_lds<P>(a.ld + row0 + 2 * P * lane, ld, 2 * P, al_ld);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (!kNoMem && t + nw < nfull) wave_dma<D, TR>(sm, a.in + (int64_t)(t + nw) * TF, lane);
+      if (!kNoMem && t + nw < nfull) wave_dma<D, TR>(sm, in + (int64_t)(t + nw) * TF, lane);
     } else {
       if constexpr (kStage == 0) {
 #pragma unroll
@@ -716,8 +723,8 @@ __global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) v
       for (int p = 0; p < P; ++p)
 #pragma unroll
         for (int k = 0; k < D; ++k) {
-          v[p][R<D, O>(k)].x = 2 * p < nr ? a.in[(r + 2 * p) * D + k] : 0.f;
-          v[p][R<D, O>(k)].y = 2 * p + 1 < nr ? a.in[(r + 2 * p + 1) * D + k] : 0.f;
+          v[p][R<D, O>(k)].x = 2 * p < nr ? in[(r + 2 * p) * D + k] : 0.f;
+          v[p][R<D, O>(k)].y = 2 * p + 1 < nr ? in[(r + 2 * p + 1) * D + k] : 0.f;
         }
     };
     if (odd) load_rows(std::true_type{});
@@ -740,7 +747,8 @@ __global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) v
   }
 }
 
-using KFn = void (*)(const float*, const int32_t*, const int32_t*, const float*, KArgs);
+using KFn = void (*)(const float*, int64_t, const float*, const int32_t*, const int32_t*,
+                     const float*, KArgs);
 
 // one instantiation and the rows of its wave tile
 struct KV {
@@ -881,7 +889,6 @@ int sgpr_run(const Shape& s, const void* prepared, const float* in, float* out, 
   const int32_t* flags = inv_q + s.L * s.D;
   const float* W = reinterpret_cast<const float*>(base + idx_bytes(s)) + s.sp_region;
   KArgs a{};
-  a.in = in;
 #ifdef CNF_AB_NO_Z  // A/B timing only: outputs not written
   out = nullptr;
 #endif
@@ -895,13 +902,12 @@ int sgpr_run(const Shape& s, const void* prepared, const float* in, float* out, 
   a.part = loss_ws ? loss_ws + 4 : nullptr;
   a.ctr = reinterpret_cast<uint32_t*>(loss_ws);
   a.terms = loss_terms;
-  a.B = B;
   a.L = s.L;
   a.kind = kind;
   a.det = det;
   const int64_t nblk = grid_for(*k, s, B);
-  hipLaunchKernelGGL(k->fn, dim3((unsigned)nblk), dim3(kWaves * 64), lds_bytes(s, *k), st, W,
-                     inverse ? inv_q : fwd_q, flags, log_priors, a);
+  hipLaunchKernelGGL(k->fn, dim3((unsigned)nblk), dim3(kWaves * 64), lds_bytes(s, *k), st, in, B,
+                     W, inverse ? inv_q : fwd_q, flags, log_priors, a);
   // the block-order sum of the loss records: a one-block follow-up launch.
   // (A last-block hand-off inside k_sgpr -- agent-scope fence + counter per
   // block -- measured 67.6 vs 35.6 us per 2^20-row call while z was written
