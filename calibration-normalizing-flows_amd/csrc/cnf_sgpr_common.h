@@ -163,25 +163,72 @@ __device__ __forceinline__ void read_pairs(const float* sm, int lane, f2 (&v)[P]
       v[p][REV ? D - 1 - k : k] = f2{b[2 * p * D + k], b[(2 * p + 1) * D + k]};
 }
 
-// read_pairs with the ds_read2_b32 issued as asm straight into the pair
-// registers, then ONE wait that carries every pair as an in/out operand, so
-// no use of a row can be scheduled above it.  (The compiler merged the plain
-// loads into ds_read_b128 of four features of one row, and regrouping those
-// into pairs cost ~15 v_mov per tile.)
+// ds_read2_pairs<D>(base, o): o[k] = (lds[base + k], lds[base + D + k]) for
+// k < D -- D ds_read2_b32 straight into the pair registers AND the wait for
+// them in ONE asm statement, so the compiler never sees a pair register
+// before its data has landed (a wait in a separate statement would leave it
+// free to copy or spill a register between the read and the wait).  Outputs
+// are early-clobber: no pair may share the address register.  One
+// specialisation per D (an asm string's length is fixed).
+#define CNF_RP_L(k) "ds_read2_b32 %" #k ", %[b] offset0:" #k " offset1:%[d]+" #k "\n\t"
+#define CNF_RP_O(k) "=&v"(o[k])
+#define CNF_RPL2 CNF_RP_L(0) CNF_RP_L(1)
+#define CNF_RPL3 CNF_RPL2 CNF_RP_L(2)
+#define CNF_RPL4 CNF_RPL3 CNF_RP_L(3)
+#define CNF_RPL5 CNF_RPL4 CNF_RP_L(4)
+#define CNF_RPL6 CNF_RPL5 CNF_RP_L(5)
+#define CNF_RPL7 CNF_RPL6 CNF_RP_L(6)
+#define CNF_RPL8 CNF_RPL7 CNF_RP_L(7)
+#define CNF_RPL9 CNF_RPL8 CNF_RP_L(8)
+#define CNF_RPL10 CNF_RPL9 CNF_RP_L(9)
+#define CNF_RPL11 CNF_RPL10 CNF_RP_L(10)
+#define CNF_RPL12 CNF_RPL11 CNF_RP_L(11)
+#define CNF_RPL13 CNF_RPL12 CNF_RP_L(12)
+#define CNF_RPL14 CNF_RPL13 CNF_RP_L(13)
+#define CNF_RPL15 CNF_RPL14 CNF_RP_L(14)
+#define CNF_RPL16 CNF_RPL15 CNF_RP_L(15)
+#define CNF_RPO2 CNF_RP_O(0), CNF_RP_O(1)
+#define CNF_RPO3 CNF_RPO2, CNF_RP_O(2)
+#define CNF_RPO4 CNF_RPO3, CNF_RP_O(3)
+#define CNF_RPO5 CNF_RPO4, CNF_RP_O(4)
+#define CNF_RPO6 CNF_RPO5, CNF_RP_O(5)
+#define CNF_RPO7 CNF_RPO6, CNF_RP_O(6)
+#define CNF_RPO8 CNF_RPO7, CNF_RP_O(7)
+#define CNF_RPO9 CNF_RPO8, CNF_RP_O(8)
+#define CNF_RPO10 CNF_RPO9, CNF_RP_O(9)
+#define CNF_RPO11 CNF_RPO10, CNF_RP_O(10)
+#define CNF_RPO12 CNF_RPO11, CNF_RP_O(11)
+#define CNF_RPO13 CNF_RPO12, CNF_RP_O(12)
+#define CNF_RPO14 CNF_RPO13, CNF_RP_O(13)
+#define CNF_RPO15 CNF_RPO14, CNF_RP_O(14)
+#define CNF_RPO16 CNF_RPO15, CNF_RP_O(15)
+template <int D>
+__device__ __forceinline__ void ds_read2_pairs(uint32_t base, f2* o);
+#define CNF_RPW(D)                                                                   \
+  template <>                                                                        \
+  __device__ __forceinline__ void ds_read2_pairs<D>(uint32_t base, f2 * o) {         \
+    asm volatile(CNF_RPL##D "s_waitcnt lgkmcnt(0)"                                   \
+                 : CNF_RPO##D                                                        \
+                 : [b] "v"(base), [d] "i"(D)                                         \
+                 : "memory");                                                        \
+  }
+CNF_RPW(2) CNF_RPW(3) CNF_RPW(4) CNF_RPW(5) CNF_RPW(6) CNF_RPW(7) CNF_RPW(8) CNF_RPW(9)
+CNF_RPW(10) CNF_RPW(11) CNF_RPW(12) CNF_RPW(13) CNF_RPW(14) CNF_RPW(15) CNF_RPW(16)
+#undef CNF_RPW
+
+// read_pairs with the ds_read2_b32 issued straight into the pair registers
+// and waited for in the same asm statement (ds_read2_pairs).  (The compiler
+// merged the plain loads into ds_read_b128 of four features of one row, and
+// regrouping those into pairs cost ~15 v_mov per tile.)
 template <int D, bool REV = false>
 __device__ __forceinline__ void read_pairs_wait(const float* sm, int lane, f2 (&v)[1][D]) {
-  static_assert(2 * D <= 256, "ds_read2_b32 dword offsets are 8-bit");
+  static_assert(D >= 2 && D <= 16, "ds_read2_pairs is specialised for 2 <= D <= 16");
   typedef __attribute__((address_space(3))) const float lds_f;
   const uint32_t base = (uint32_t)(uintptr_t)(lds_f*)(sm + 2 * D * lane);
+  f2 o[D];
+  ds_read2_pairs<D>(base, o);
 #pragma unroll
-  for (int k = 0; k < D; ++k)
-    asm volatile("ds_read2_b32 %0, %1 offset0:%2 offset1:%3"
-                 : "=v"(v[0][REV ? D - 1 - k : k])
-                 : "v"(base), "i"(k), "i"(D + k)
-                 : "memory");
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-  for (int k = 0; k < D; ++k) asm volatile("" : "+v"(v[0][k]));
+  for (int k = 0; k < D; ++k) v[0][REV ? D - 1 - k : k] = o[k];
 }
 
 // Coalesced tile stores.  A lane's 2P output rows sit 2*P*D floats apart from

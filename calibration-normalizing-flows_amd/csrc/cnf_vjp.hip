@@ -587,11 +587,7 @@ VFn2 pick_v2(const V2Entry* e, const Shape& s, bool loss) {
   return e->fn[s.scale ? 1 : 0][loss ? 1 : 0][s.any_perm ? 1 : 0];
 }
 
-// (covers both stage layouts: the pipelined one overlays the input tile)
-size_t lds_v2(const Shape& s) {
-  const size_t pipe = (size_t)32 * v2::kV2SP, tile = (size_t)kV2TR * s.D;
-  return (tile + 32 * kV2SS > pipe ? tile + 32 * kV2SS : pipe) * 4;
-}
+size_t lds_v2(const Shape& s) { return (size_t)(kV2TR * s.D + 32 * kV2SS) * 4; }
 
 // persistent grid: as many one-wave blocks as fit, at most one per tile
 int64_t grid_v2(const Shape& s, VFn2 fn, int64_t B) {

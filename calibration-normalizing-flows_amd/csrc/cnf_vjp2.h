@@ -326,79 +326,15 @@ __device__ __forceinline__ floatx4 wgrad_tile(float* st, const f2* G, const f2* 
   return acc;
 }
 
-// CNF_V2_PIPE=1 (A/B; measured 0.1796-0.1805 ms per cfg2 step against
-// 0.1778-0.1791 for the default): the dW stage holds the whole 128-row tile (G features
-// 0..15, H 16..31; lane l's rows at columns l and 64 + l) and is software-
-// pipelined against the VALU: a net's stage is written, then independent VALU
-// work runs (the other net's back-propagation, or the next layer's recompute)
-// while the 62 stores drain, and only then is it folded.  The fold streams its
-// operands with the next float4 pair in flight behind each 4-MFMA group.
-// 0 (default) = the 64-row stage folded right after it is written
-// (wgrad_tile): the block's second wave already covers those LDS waits.
-#ifndef CNF_V2_PIPE
-#define CNF_V2_PIPE 0
-#endif
 #ifndef CNF_V2_HLATE
 #define CNF_V2_HLATE 1  // the dW stack's 2^64 on h' applied once per wave (below)
 #endif
 #ifndef CNF_V2_TLATE
 #define CNF_V2_TLATE 0  // A/B: the t-net recompute after the s-net's backward step
 #endif
-// Stage row stride 136 floats: a lane (i = l%16, q = l/16) reads float4 c of
-// feature i at i*136 + 16c + 4q, so every 16-lane group of ds_read_b128 lands
-// on 64 distinct banks (136/4 = 34 = 2 mod 16 puts the q-odd lanes on the odd
-// 4-bank slots), and 64 consecutive lanes store 64 consecutive floats.
-constexpr int kV2SP = 136;
 #ifndef CNF_V2_WPS
 #define CNF_V2_WPS 2  // waves per SIMD the register budget is held to
 #endif
-
-template <int GS, int HS>
-__device__ __forceinline__ void stage_put(float* st, const f2* G, const f2* H, int lane) {
-#pragma unroll
-  for (int f = 0; f < GS; ++f) {
-    st[f * kV2SP + lane] = G[f].x;
-    st[f * kV2SP + 64 + lane] = G[f].y;
-  }
-#pragma unroll
-  for (int f = 0; f < HS; ++f) {
-    st[(16 + f) * kV2SP + lane] = H[f].x;
-    st[(16 + f) * kV2SP + 64 + lane] = H[f].y;
-  }
-}
-
-// acc += G^T H over the staged 128 rows: 32 MFMA steps, lane (i, q) feeding
-// rows 16c + 4q + e (c < 8, e < 4) of feature i.  The reads are inline asm so
-// that the next float4 pair is issued before the current group's MFMAs; each
-// pair is waited for with a counted lgkmcnt (LDS returns in order; an SMEM
-// load in between only makes the count wait longer) and laundered through an
-// empty asm after the wait, so no MFMA can be scheduled above it.
-__device__ __forceinline__ floatx4 stage_fold(const float* st, int lane, floatx4 acc) {
-  typedef __attribute__((address_space(3))) float lds_f;
-  const uint32_t a = (uint32_t)(uintptr_t)(lds_f*)(st + (lane & 15) * kV2SP + 4 * (lane >> 4));
-  constexpr int kB = 16 * kV2SP * 4;  // byte offset of the H features
-  floatx4 A[2], Bv[2];
-  asm volatile("ds_read_b128 %0, %1" : "=v"(A[0]) : "v"(a) : "memory");
-  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(Bv[0]) : "v"(a), "i"(kB) : "memory");
-  static_for<0, 8>([&](auto C) __attribute__((always_inline)) {
-    constexpr int c = decltype(C)::value, cur = c & 1, nxt = cur ^ 1;
-    if constexpr (c < 7) {
-      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(A[nxt]) : "v"(a), "i"(64 * (c + 1))
-                   : "memory");
-      asm volatile("ds_read_b128 %0, %1 offset:%2"
-                   : "=v"(Bv[nxt]) : "v"(a), "i"(kB + 64 * (c + 1)) : "memory");
-      asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    }
-    asm volatile("" : "+v"(A[cur]), "+v"(Bv[cur]));
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(A[cur].x, Bv[cur].x, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(A[cur].y, Bv[cur].y, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(A[cur].z, Bv[cur].z, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(A[cur].w, Bv[cur].w, acc, 0, 0, 0);
-  });
-  return acc;
-}
 
 // parameter p (state_dict order of one layer) -> (G row i, H column j) of its
 // gradient in the (layer, net) tile, or -1 when the gradient is zero by the mask
@@ -474,14 +410,8 @@ __global__ __launch_bounds__(64, CNF_V2_WPS) void k_vjp2(const float* __restrict
   constexpr int TF = kV2TR * D;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* tile = smem;        // [TF] input rows
-#if CNF_V2_PIPE
-  // the tile is done with (forward read, seed) before the first stage write
-  float* st = smem;          // [32][kV2SP] G / H stage of all 128 rows
-  constexpr int kStage = 32 * kV2SP;
-#else
   float* st = smem + TF;     // [32][kV2SS] G / H stage
   constexpr int kStage = 32 * kV2SS;
-#endif
   const int lane = threadIdx.x;
   const int64_t B = a.B;
   const int L = a.L;
@@ -663,15 +593,12 @@ __global__ __launch_bounds__(64, CNF_V2_WPS) void k_vjp2(const float* __restrict
         asm volatile("ds_add_f32 %0, %1" ::"v"(tb + 4u * yy[0]), "v"(dy[0]) : "memory");
         asm volatile("ds_add_f32 %0, %1 offset:%2" ::"v"(tb + 4u * yy[1]), "v"(dy[1]), "i"(4 * D)
                      : "memory");
+        {  // the reads and their wait in one asm statement (ds_read2_pairs)
+          f2 o[D];
+          ds_read2_pairs<D>(tb, o);
 #pragma unroll
-        for (int j = 0; j < D; ++j)
-          asm volatile("ds_read2_b32 %0, %1 offset0:%2 offset1:%3"
-                       : "=v"(g[R<D, O>(j)])
-                       : "v"(tb), "i"(j), "i"(D + j)
-                       : "memory");
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-        for (int j = 0; j < D; ++j) asm volatile("" : "+v"(g[R<D, O>(j)]));
+          for (int j = 0; j < D; ++j) g[R<D, O>(j)] = o[j];
+        }
       } else
 #endif
       if constexpr (LOSS) {
@@ -795,13 +722,6 @@ __global__ __launch_bounds__(64, CNF_V2_WPS) void k_vjp2(const float* __restrict
       if constexpr (NETS == 2) {
         f2 sh1[H1 ? H1 : 1], sh2[H2 ? H2 : 1], sv[DT];
         vnet_fwd_sp<S, NC>(ws, c, sh1, sh2, sv);  // sv = log2(e) s
-#if CNF_V2_PIPE
-        // layer l+1's t-net stage, written at the end of its backward step,
-        // drained behind this layer's recompute
-        if constexpr (l + 1 < kV2LMax) {
-          if (l + 1 < L) acc[l + 1][1] = stage_fold(st, lane, acc[l + 1][1]);
-        }
-#endif
         f2 gs[DT];
 #pragma unroll
         for (int j = 0; j < DT; ++j) {
@@ -819,17 +739,8 @@ __global__ __launch_bounds__(64, CNF_V2_WPS) void k_vjp2(const float* __restrict
         for (int m = 0; m < H1; ++m) H[DC + m] = sh1[m] * splat(kHs, f2{});
 #pragma unroll
         for (int m = 0; m < H2; ++m) H[DC + H1 + m] = sh2[m] * splat(kHs, f2{});
-#if CNF_V2_PIPE
-        stage_put<GS, HS>(st, G, H, lane);  // folded after the t-net's VALU below
-#else
         acc[l][0] = wgrad_tile<GS, HS>(st, G, H, lane, acc[l][0]);
-#endif
       }
-#if CNF_V2_PIPE
-      if constexpr (NETS == 1 && l + 1 < kV2LMax) {  // (see the s-net branch)
-        if (l + 1 < L) acc[l + 1][0] = stage_fold(st, lane, acc[l + 1][0]);
-      }
-#endif
       {  // t-net: d/dt = g_T (before the e^s scaling of the s-net branch)
 #if CNF_V2_TLATE
         // recomputed only now: th1 / th2 are not live across the s-net's step
@@ -844,18 +755,11 @@ __global__ __launch_bounds__(64, CNF_V2_WPS) void k_vjp2(const float* __restrict
 #pragma unroll
           for (int f = 0; f < GS; ++f) G[f] *= keep;
         }
-#if CNF_V2_PIPE
-        if constexpr (NETS == 2) acc[l][0] = stage_fold(st, lane, acc[l][0]);
-#endif
 #pragma unroll
         for (int m = 0; m < H1; ++m) H[DC + m] = th1[m] * splat(kHs, f2{});
 #pragma unroll
         for (int m = 0; m < H2; ++m) H[DC + H1 + m] = th2[m] * splat(kHs, f2{});
-#if CNF_V2_PIPE
-        stage_put<GS, HS>(st, G, H, lane);  // folded by layer l - 1 (or after the sweep)
-#else
         acc[l][NETS - 1] = wgrad_tile<GS, HS>(st, G, H, lane, acc[l][NETS - 1]);
-#endif
       }
 #pragma unroll
       for (int j = 0; j < DT; ++j) {
@@ -869,9 +773,6 @@ __global__ __launch_bounds__(64, CNF_V2_WPS) void k_vjp2(const float* __restrict
       constexpr int l = kV2LMax - 1 - decltype(I)::value;
       if (l < L) bwd(std::integral_constant<int, l>{});
     });
-#if CNF_V2_PIPE
-    acc[0][NETS - 1] = stage_fold(st, lane, acc[0][NETS - 1]);  // layer 0's t-net
-#endif
     if (a.dx) {
 #pragma unroll
       for (int j = 0; j < D; ++j) {

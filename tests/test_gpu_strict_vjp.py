@@ -189,3 +189,104 @@ def test_strict_inverse_workspace_is_reported():
     st = _lib.lib().cnf_vjp_inverse_workspace_bytes(ctypes.byref(f._native_stack().desc),
                                                     ctypes.c_int64(4), ctypes.byref(n))
     assert st == 0 and n.value > 0
+
+
+# Strict stacks off the D=4 fixture's narrow path: the MFMA-tile
+# family's strict geometry (Op = r8(D), Cp = r8(D+1), the zero columns of the
+# coupling epilogues) serves wide D, odd D, shift-only (NICE) and random_flip
+# stacks.  Synthetic weights N(0, 0.3) (0.05 at D=40); where the stack has an s-net, layer
+# 0's s-net is pushed to overflow exp(s) at its last output in about half of
+# the rows (inputs x 8), so NaN / inf and finite rows mix.
+_SYN = {
+    "wide_d40": dict(D=40, hidden=[64], L=3, scale=True, shift=True, random_flip=False),
+    "odd_d7": dict(D=7, hidden=[5, 5], L=3, scale=True, shift=True, random_flip=False),
+    "nice_d10": dict(D=10, hidden=[5, 5], L=3, scale=False, shift=True, random_flip=False),
+    "flip_d10": dict(D=10, hidden=[5, 5], L=3, scale=True, shift=True, random_flip=True),
+}
+
+
+def _syn_case(name, B=96):
+    meta = dict(_SYN[name], seed=11)
+    np.random.seed(meta["seed"])
+    torch.manual_seed(0)
+    from flows.flows import Flow, NvpCouplingLayer
+    f = Flow([NvpCouplingLayer(meta["D"], list(meta["hidden"]), scale=meta["scale"],
+                               shift=meta["shift"], random_flip=meta["random_flip"])
+              for _ in range(meta["L"])])
+    g = torch.Generator().manual_seed(5)
+    state = {}
+    for k, v in f.state_dict().items():
+        v = v.clone()
+        if v.dtype.is_floating_point and ("weight" in k or "bias" in k):
+            v = torch.randn(v.shape, generator=g) * (0.3 if meta["D"] <= 16 else 0.05)
+        state[k] = v.numpy()
+    x = torch.randn(B, meta["D"], generator=g) * 8.0
+    y = torch.randint(0, meta["D"], (B,), generator=g)
+    if meta["scale"]:
+        # the last s output's pre-activation u = w . h + b over the batch (h: the
+        # input of layer 0's last s Linear), rescaled so that u > 89 (fp32 exp
+        # overflows above 88.72) in about half of the rows
+        wk = [k for k in state if k.startswith("layers.0.s.") and k.endswith("weight")][-1]
+        bk = wk[:-len("weight")] + "bias"
+        ff = build_flow(meta, state, "cpu")
+        last = [m for m in ff.layers[0].s.modules() if isinstance(m, torch.nn.Linear)][-1]
+        got = {}
+        def keep_input(m, i, o):
+            got.setdefault("h", i[0].detach())  # (returns None: the output stays)
+        hk = last.register_forward_hook(keep_input)
+        with torch.no_grad():
+            ff(x)
+        hk.remove()
+        u = got["h"] @ torch.from_numpy(state[wk][-1]).float()
+        a = 40.0 / (float(u.std()) + 1e-6)
+        state[wk] = state[wk].copy()
+        state[bk] = state[bk].copy()
+        state[wk][-1] *= a
+        state[bk][-1] = 89.0 - a * float(u.median())
+    return meta, state, x, y
+
+
+@pytest.mark.parametrize("name", sorted(_SYN))
+@pytest.mark.parametrize("objective", ["loss", "zs"])
+def test_strict_vjp_off_the_narrow_path(name, objective):
+    meta, state, x, y = _syn_case(name)
+    obj = _loss if objective == "loss" else _zs_objective
+    ref_out, ref = _cpu_grads(meta, state, x, y, obj)
+    f = build_flow(meta, state, DEV, strict_nan=True)
+    assert f._native_stack().has_native_vjp(), "strict stacks must have a native reverse mode"
+    xx = x.to(DEV).requires_grad_(True)
+    n0 = engine.stats["vjp"]
+    out = obj(f, xx, y.to(DEV))
+    ps = [p for p in f.parameters() if p.requires_grad]
+    got = torch.autograd.grad(out, ps + [xx], allow_unused=True)
+    torch.cuda.synchronize()
+    if not engine.USE_TORCH_OPS:
+        assert engine.stats["vjp"] > n0, "native cnf_vjp did not run"
+    if meta["scale"] and objective == "zs":  # the case must mix NaN / inf and finite rows
+        bad = ~torch.isfinite(ref[-1]).all(1)
+        assert bad.any() and not bad.all(), (name, int(bad.sum()))
+    _same(out, ref_out, "objective")
+    for i, (gg, r) in enumerate(zip(got, ref)):
+        _same(torch.zeros_like(r) if gg is None else gg, r, "grad %d" % i)
+
+
+@pytest.mark.parametrize("name", sorted(_SYN))
+def test_strict_inverse_vjp_off_the_narrow_path(name):
+    meta, state, x, _ = _syn_case(name)
+    z = x / 8.0
+    f_cpu = build_flow(meta, state, "cpu", strict_nan=True)
+    zc = z.clone().requires_grad_(True)
+    ref_out = _inv_xs_objective(f_cpu, zc)
+    ps_cpu = [p for p in f_cpu.parameters() if p.requires_grad]
+    ref = torch.autograd.grad(ref_out, ps_cpu + [zc], allow_unused=True)
+    ref = [torch.zeros_like(p) if g is None else g for g, p in zip(ref, ps_cpu + [zc])]
+    f = build_flow(meta, state, DEV, strict_nan=True)
+    assert f._native_stack().has_native_vjp_inverse()
+    zz = z.to(DEV).requires_grad_(True)
+    out = _inv_xs_objective(f, zz)
+    ps = [p for p in f.parameters() if p.requires_grad]
+    got = torch.autograd.grad(out, ps + [zz], allow_unused=True)
+    torch.cuda.synchronize()
+    _same(out, ref_out.detach(), "objective")
+    for k, (g, r) in enumerate(zip(got, ref)):
+        _same(torch.zeros_like(r) if g is None else g, r, "grad %d" % k)
