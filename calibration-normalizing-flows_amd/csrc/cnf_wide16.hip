@@ -428,10 +428,14 @@ __device__ __forceinline__ void row_centre16(float* st, int S, int lane) {
   constexpr int HF = (D + 1) / 2;
   const int row = lane & 31, f0 = (lane >> 5) * HF, f1 = f0 + HF < D ? f0 + HF : D;
   float* r = st + row * S;
-  float s = 0.f;
-  for (int f = f0; f < f1; ++f) s += r[f];
+  // the row mean summed in fp64 and rounded once: the mean torch's fp32
+  // reduction approximates (its order is not reproducible here, and a
+  // 100-wide flow at N(0, 0.1) turns one ulp of the mean into 1e-2 of the
+  // probabilities; tests/test_gpu_parity.py, wide predict at N(0, 0.1))
+  double s = 0.0;
+  for (int f = f0; f < f1; ++f) s += (double)r[f];
   s += __shfl_xor(s, 32);
-  const float mu = s * (1.f / D);
+  const float mu = (float)(s / D);
   for (int f = f0; f < f1; ++f) r[f] -= mu;
 }
 template <int D>

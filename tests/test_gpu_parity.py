@@ -483,6 +483,42 @@ def test_fused_predict_matches_reference_formula(D, hidden, L, flip):
     assert np.max(np.abs(probs.cpu().numpy() - ref)) <= 1e-5
 
 
+def test_fused_wide_predict_at_n01_within_the_references_own_fp32_error():
+    """The wide fused predict (k_wide16's predict mode) at N(0, 0.1) weights,
+    where the 100-wide flow amplifies last-ulp input differences: the fused
+    probabilities must be as close to the fp64 evaluation of the reference
+    formula (calibrators.py:40-44, 350-352; centring, flow and softmax all in
+    fp64 on the CPU) as the reference's own fp32 evaluation is, with 1e-5 as
+    the floor: tol = max(1e-5, 2 x |fp32 ref - fp64 ref|)."""
+    D, hidden, L = 100, [100, 100], 2
+    f = _make_flow(D, L, hidden, 0.1, 4)
+    stack = f._native_stack()
+    g = torch.Generator(device=DEV).manual_seed(8)
+    x = torch.randn(5000, D, device=DEV, generator=g) * 3 + 1
+    pri = torch.rand(D, generator=torch.Generator().manual_seed(1)).double() + 0.1
+    lp = torch.log(pri / pri.sum())
+    n0 = engine.stats["predict"]
+    probs = stack.predict(x, lp).cpu().double()
+    assert engine.stats["predict"] == n0 + 1
+    import copy
+
+    def formula(flow, xx):
+        with torch.no_grad():
+            z, _ = flow.transform(xx - xx.mean(dim=1, keepdim=True))
+        p = torch.softmax(z.double(), dim=1).cpu()
+        return torch.softmax(torch.log(p + 1e-7) - lp, dim=1)
+    ref32 = formula(copy.deepcopy(f).cpu(), x.cpu())
+    ref64 = formula(copy.deepcopy(f).cpu().double(), x.cpu().double())
+    err_ref = (ref32 - ref64).abs().max().item()
+    err_gpu = (probs - ref64).abs().max().item()
+    tol = max(1e-5, 2 * err_ref)
+    import conftest
+    conftest.RECORDS.setdefault("predict_errors", []).append(
+        {"test": "wide_predict_n01", "gpu_vs_fp64": err_gpu, "ref_fp32_vs_fp64": err_ref,
+         "tol": tol})
+    assert err_gpu <= tol, (err_gpu, err_ref)
+
+
 @pytest.mark.parametrize("name", ["g2_nvp_d10_n02", "g6_d10_randflip", "g3_nvp_d100_n003",
                                   "g1_nice_d3_n02"])
 @pytest.mark.parametrize("via_ops", [True, False])
