@@ -666,6 +666,76 @@ __device__ __forceinline__ void wdwg_chunks(const DwJob& j, float* sm, int w, in
   }
 }
 
+// The same chunk loop with the job's (row tile, column tile) pairs dealt to
+// the four waves round-robin (pair p = NTH t + c to wave p % 4) instead of
+// whole row tiles: a 7-row-tile job gave waves 0-2 two row tiles and wave 3
+// one (each block's fourth SIMD half idle), a 1-row-tile job all its work to
+// wave 0.  A wave reads the operand tiles its pairs touch (unused reads are
+// dropped by the compiler) and writes its own cells.
+#ifndef CNF_WDWG_RR
+#define CNF_WDWG_RR 1
+#endif
+template <int NTG, int NTH, int W>
+__device__ __forceinline__ void wdwg_rr(const DwJob& j, const DwArgs& da, float* sm, int lane,
+                                        int64_t r0, int nch) {
+  constexpr int TPC = NTG + NTH, NPJ = NTG * NTH;
+  constexpr int NP = NPJ > W ? (NPJ - W + 3) / 4 : 0;  // this wave's pairs
+  const int64_t ldg = j.ldg, ldh = j.ldh;
+  const int i = lane & 15, kq = lane >> 4;
+  f4 acc[NP > 0 ? NP : 1];
+#pragma unroll
+  for (int m = 0; m < NP; ++m) acc[m] = f4{};
+  auto dma = [&](int c, int stg) {
+    const float* gsrc = j.G + ((r0 >> 5) + c) * 32 * ldg;
+    const float* hsrc = j.H + ((r0 >> 5) + c) * 32 * ldh;
+    float* dst = sm + stg * TPC * 512;
+#pragma unroll
+    for (int k0 = 0; k0 < 2 * TPC; k0 += 4) {  // 1 KiB pieces; piece k0 + W is this wave's
+      const int k = k0 + W;
+      if (k < 2 * TPC) {
+        const float* src = k < 2 * NTG ? gsrc + k * 256 : hsrc + (k - 2 * NTG) * 256;
+        __builtin_amdgcn_global_load_lds(const_cast<float*>(src) + lane * 4, dst + k * 256, 16, 0, 0);
+      }
+    }
+  };
+  dma(0, 0);
+  for (int c = 0; c < nch; ++c) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of chunk c
+    __syncthreads();  // everyone's pieces landed; everyone is done with chunk c - 1
+    if (c + 1 < nch) dma(c + 1, (c + 1) & 1);
+    const float* S = sm + (c & 1) * TPC * 512 + lane;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {  // 4 rows per k-step: row 4s + kq of the 32-row block
+      float a[NTG], b[NTH];
+#pragma unroll
+      for (int t = 0; t < NTG; ++t) a[t] = S[t * 512 + s * 64];
+#pragma unroll
+      for (int q = 0; q < NTH; ++q) b[q] = S[(NTG + q) * 512 + s * 64];
+#pragma unroll
+      for (int m = 0; m < NP; ++m) {
+        const int p = W + 4 * m;
+        acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[p / NTH], b[p % NTH], acc[m], 0, 0, 0);
+      }
+    }
+  }
+  // lane (i, kq), register q of pair (t, c): dW row slot 16 t + 4 kq + q,
+  // column slot 16 c + i, each mapped to its unit
+  float* out = da.partials + (int64_t)blockIdx.x * da.PS;
+#pragma unroll
+  for (int m = 0; m < NP; ++m) {
+    const int p = W + 4 * m, t = p / NTH, c = p % NTH;
+    const int k = slot_unit(16 * c + i);
+    if (k > j.K) continue;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int nn = slot_unit(16 * t + 4 * kq + q);
+      if (nn >= j.N) continue;
+      if (k < j.K) out[j.woff + (int64_t)nn * j.wld + k] = acc[m][q];
+      else out[j.boff + nn] = acc[m][q];
+    }
+  }
+}
+
 // the (G tiles, H tiles) classes with an instantiation: the weight gradients
 // of k_wide16's table (cfg4: (7, 4), (7, 7), (4, 7))
 #define CNF_WDWG_CLASSES(X) X(7, 4) X(7, 7) X(4, 7) X(4, 4) X(4, 2) X(4, 5) X(1, 5)
@@ -696,6 +766,13 @@ __global__ __launch_bounds__(256, 2) void k_wdw16g(DwArgs da) {
   // barriers) whatever its row-tile count
 #define CNF_WDWG_RUN(A, B)                                                    \
   if (ntg == A && nth == B) {                                                 \
+    if (CNF_WDWG_RR && A % 4 != 0) {                                          \
+      if (w == 0) wdwg_rr<A, B, 0>(j, da, sm, lane, r0, nch);                 \
+      else if (w == 1) wdwg_rr<A, B, 1>(j, da, sm, lane, r0, nch);            \
+      else if (w == 2) wdwg_rr<A, B, 2>(j, da, sm, lane, r0, nch);            \
+      else wdwg_rr<A, B, 3>(j, da, sm, lane, r0, nch);                        \
+      return;                                                                 \
+    }                                                                         \
     if (nr == 2) wdwg_chunks<A, B, 2>(j, sm, w, lane, r0, nch, acc);           \
     else if (nr == 1) wdwg_chunks<A, B, 1>(j, sm, w, lane, r0, nch, acc);      \
     else wdwg_chunks<A, B, 0>(j, sm, w, lane, r0, nch, acc);                   \

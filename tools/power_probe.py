@@ -1,8 +1,9 @@
 """Board power and clocks while the cfg2 bench pass runs back to back: is the
 device at its power cap (the shader clock then falls as memory traffic is
 added, tools/sgpr_trace.py clock_ghz)?  Samples `rocm-smi` (read-only) idle
-and under load.  usage: power_probe.py [loss|forward|train] [seconds] [B]
-(train: the fused calibrator step, cnf_loss_vjp + reduction)."""
+and under load.  usage: power_probe.py [loss|forward|train|train4] [seconds] [B]
+(train / train4: the fused calibrator step, cnf_loss_vjp + reduction, on cfg2 /
+cfg4)."""
 import json
 import os
 import subprocess
@@ -31,12 +32,14 @@ def smi():
 
 
 dev = torch.device("cuda:0")
-if mode == "train":
+if mode in ("train", "train4"):
     from cnf_hip import vjp as V
+    if mode == "train4" and B == 1 << 20:
+        B = bench.WORKLOADS["cfg4"]["B"]
 
     class _Train:
         def __init__(self):
-            w = bench.WORKLOADS["cfg2"]
+            w = bench.WORKLOADS["cfg2" if mode == "train" else "cfg4"]
             self.stack = bench.make_flow(w, dev)._native_stack()
             self.x, self.y = bench.synthetic_logits(B, w["D"], dev, 4321)
 
@@ -64,7 +67,7 @@ th.start()
 t0 = time.perf_counter()
 t_end = t0 + secs
 n = 0
-per = max(1, ((200 if mode != "train" else 25) << 20) // B)
+per = {"train": max(1, (25 << 20) // B), "train4": 4}.get(mode, max(1, (200 << 20) // B))
 while time.perf_counter() < t_end:
     for _ in range(per):
         r.step()
