@@ -43,9 +43,9 @@
 //     and the wave stores the tile lane-linear with streaming 16-B stores, each
 //     instruction 1 KiB contiguous; the next tile's LDS-DMA is issued once the
 //     staged rows have been read back (kStage 1 below);
-//   * a persistent grid (CUs x resident blocks) walks the tiles wave by wave;
-//     s_setprio by tiles remaining (longest-remaining-first) keeps the SIMDs'
-//     oldest-first arbitration from leaving a long single-wave tail.
+//   * a persistent grid (CUs x resident blocks) walks the tiles wave by wave
+//     (priority schedules by tiles remaining were measured and lost:
+//     CNF_SGPR_PRIO, off).
 // Every variant is compile-time (mode, random_flip, every-layer stores), so
 // the hot loop has no data-dependent branches and no scratch.
 #include <hip/hip_runtime.h>

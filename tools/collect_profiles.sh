@@ -19,5 +19,8 @@ for spec in "cfg2 loss k_sgpr 1048576" "cfg2 all k_valu 1048576" "cfg2 train k_v
   python tools/pmc_summary.py $dir $3 > profiles/${TAG}_pmc_${sfx}.txt
   python tools/pmc_traffic.py $dir profiles/${TAG}_traffic_${sfx}.json $1 $4 $3 > /dev/null
 done
+for rec in inverse_errors predict_errors; do
+  [ -f gpurun_out/$rec.jsonl ] && cp gpurun_out/$rec.jsonl profiles/${TAG}_$rec.jsonl
+done
 grep '^{"metric"' gpurun_out/bench.log | tail -1 >> profiles/${TAG}_bench.jsonl
 ls profiles/ | grep "^${TAG}_"

@@ -20,7 +20,7 @@ run() {
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
 }
 run smoke 400 python -c "import __graft_entry__ as g; g.smoke()"
-TAILN=12 run pytest_gpu 900 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread
+TAILN=12 CNF_RECORD_DIR=gpurun_out run pytest_gpu 900 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread
 TAILN=2 run bench 600 python bench.py
 [ -n "$QUICK" ] && exit 0
 run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python bench.py --steps 100 --no-cpu-baseline --no-variants
