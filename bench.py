@@ -8,8 +8,11 @@ the batch's calibration NLL (cnf_forward_loss through the C ABI: writes the
 final z [B,10] and log-det [B], and the sums of the per-row loss / ce / ld --
 the eval pass of TorchFlowCalibrator.fit, calibrators.py:297-317).  With N>1
 ranks every rank runs its own 2^20-vector shard (weak scaling: 8M vectors at
-N=8 = configs[2]) and the step ends with the RCCL all-reduce of the shard's
-3 NLL sums (configs[2]); at N=1 there is nothing to reduce.
+N=8 = configs[2]) and every batch's 3 NLL sums are summed across ranks by RCCL
+over xGMI (configs[2]), bucketed: the sums of NLL_BUCKET consecutive batches
+go in one all-reduce (a 12-B all-reduce is pure latency, ~14 us even on one
+rank, half a step), the last partial bucket before the timed region closes;
+at N=1 there is nothing to reduce.
 
 Inputs are resident in HBM before timing; the step rotates through enough
 distinct input/output buffers (>= --rotate-gb) that the 256 MB Infinity Cache
@@ -146,10 +149,12 @@ class Runner:
         self.stream = torch.cuda.current_stream(device)
         self.args = [(vp(x), vp(out), vp(ld), vp(allt), vp(y)) for (x, y, out, ld, allt) in
                      self.sets]
-        # rotating loss-term buffers: batch i's NLL all-reduce (N > 1) may still
+        # loss-term buckets: batch i writes its sums to row i % NLL_BUCKET of
+        # bucket (i // NLL_BUCKET) % 2 (two, so an overlapped all-reduce of one
+        # bucket can run while the next fills); NllAllReduce reduces whole buckets
         # be in flight while batch i+1's kernel writes the next buffer
-        self.term_bufs = [torch.zeros(3, device=device) for _ in range(TERM_BUFS)]
-        self.terms = self.term_bufs[0]
+        self.term_bufs = torch.zeros(2, NLL_BUCKET, 3, device=device)
+        self.terms = self.term_bufs[0, 0]
         if mode == "loss":
             n = ctypes.c_size_t()
             st = self.lib.cnf_forward_loss_workspace_bytes(self.desc, ctypes.c_int64(B),
@@ -167,7 +172,7 @@ class Runner:
 
     def step(self):
         a = self.args[self.i % self.nsets]
-        self.terms = self.term_bufs[self.i % TERM_BUFS]
+        self.terms = self.term_bufs[(self.i // NLL_BUCKET) % 2, self.i % NLL_BUCKET]
         self.i += 1
         blob = ctypes.c_void_p(self.blob.data_ptr())
         stream = ctypes.c_void_p(self.stream.cuda_stream)
@@ -229,38 +234,52 @@ class Runner:
         return e0.elapsed_time(e1) / 1e3, wall
 
 
-TERM_BUFS = 4
+NLL_BUCKET = 50  # batches per NLL all-reduce (bench.py --nll-bucket)
 
 
 class NllAllReduce:
-    """The one real exchange of the sharded eval (configs[2]): each batch's
-    (loss, ce, ld) sums, written by the fused kernel into the runner's current
-    terms buffer, summed across ranks by one RCCL all-reduce before the next
-    batch (the default).  overlap=True instead runs it on RCCL's own stream
-    (async_op) under the next batch's kernel: the launch stream waits for
-    all-reduce i before batch i + TERM_BUFS reuses its buffer, and drain() waits
-    for every outstanding one.  Measured on one MI355X (bench --dist-check, one
-    rank): 63.9 us per step overlapped vs 46.2 us synchronous -- the two
-    cross-stream waits per batch cost more than a 12-byte all-reduce, so the
-    synchronous form ships."""
+    """The one real exchange of the sharded eval (configs[2]): every batch's
+    (loss, ce, ld) sums, written by the fused kernel into its row of the
+    runner's current bucket, summed across ranks by RCCL -- one all-reduce per
+    full bucket of NLL_BUCKET batches (and one for the last partial bucket in
+    drain()), so every batch's global sums exist once its bucket is reduced.
+    A 12-B all-reduce per batch is all latency: measured on one MI355X (bench
+    --dist-check, one rank) 46.2 us per step against ~32 us without it.
+    overlap=True runs each bucket's all-reduce on RCCL's own stream (async_op)
+    while the other bucket fills; the launch stream waits for it before that
+    bucket is written again.  (Per batch and overlapped it measured 63.9 us per
+    step on one rank: two cross-stream waits per batch.)"""
 
     def __init__(self, runner, overlap=False):
         self.runner = runner
         self.overlap = overlap
-        self.pending = []
+        self.pending = {}
+        self.done = 0  # batches whose sums have been handed to an all-reduce
+
+    def _reduce(self, b, n):
+        t = self.runner.term_bufs[b, :n]
+        if not self.overlap:  # the launch stream waits for it
+            dist.all_reduce(t)
+            return
+        self.pending[b] = dist.all_reduce(t, async_op=True)
 
     def __call__(self):
-        if not self.overlap:  # reference point: the launch stream waits every batch
-            dist.all_reduce(self.runner.terms)
-            return
-        self.pending.append(dist.all_reduce(self.runner.terms, async_op=True))
-        if len(self.pending) >= TERM_BUFS:
-            self.pending.pop(0).wait()  # the launch stream waits for the oldest
+        i = self.runner.i  # batches launched so far
+        b = (i // NLL_BUCKET) % 2
+        if b in self.pending and i % NLL_BUCKET == 0:
+            self.pending.pop(b).wait()  # bucket b is about to be refilled
+        if i % NLL_BUCKET == 0:  # a bucket just filled
+            self._reduce((i // NLL_BUCKET - 1) % 2, NLL_BUCKET)
+            self.done = i
 
     def drain(self):
-        for w in self.pending:
+        i = self.runner.i
+        if i > self.done:  # the partial bucket
+            self._reduce((i // NLL_BUCKET) % 2, i - self.done)
+            self.done = i
+        for w in self.pending.values():
             w.wait()
-        self.pending = []
+        self.pending = {}
 
 
 def kernel_only_seconds(runner, launches):
@@ -461,6 +480,7 @@ def self_launch(n, argv):
 
 
 def main():
+    global NLL_BUCKET
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -474,13 +494,16 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--overlap-allreduce", action="store_true",
-                    help="run each batch's NLL all-reduce under the next batch's kernel")
+                    help="run each NLL bucket's all-reduce under the next bucket's kernels")
+    ap.add_argument("--nll-bucket", type=int, default=NLL_BUCKET,
+                    help="batches whose NLL sums share one all-reduce (1: one per batch)")
     ap.add_argument("--dist-check", action="store_true",
                     help="one rank through the RCCL collective path (overlapped and "
                          "synchronous all-reduce timed side by side)")
     ap.add_argument("--launch-check", action="store_true",
                     help="rank wiring only: gloo process group, no GPU (CPU test of the launcher)")
     args = ap.parse_args()
+    NLL_BUCKET = max(1, args.nll_bucket)
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         if not args.launch_check and torch.cuda.device_count() < args.gpus:
@@ -624,8 +647,8 @@ def main():
                        else "the reference's default Linear init (synthetic)"},
             "roofline": roof,
         "step": "fused forward + log-det + NLL sums (cnf_forward_loss)%s" % (
-            " + RCCL all-reduce of the NLL sums%s" % (
-                " (overlapping the next batch)" if args.overlap_allreduce else "")
+            " + RCCL all-reduce of every batch's NLL sums, %d batches per all-reduce%s" % (
+                NLL_BUCKET, " (overlapping the next bucket)" if args.overlap_allreduce else "")
             if collective else "") if mode == "loss"
             else "fused pass (cnf_%s)" % ("inverse" if w["inverse"] else "forward"),
             "cpu_baseline": cpu,
