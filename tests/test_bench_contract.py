@@ -74,3 +74,52 @@ def test_gpus_flag_must_match_launcher_world():
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1",
                           "--launch-check"], env=env, capture_output=True, text=True, timeout=300)
     assert out.returncode != 0 and "WORLD_SIZE=2" in out.stderr
+
+
+def test_nll_all_reduce_buckets_cover_every_batch_once(monkeypatch):
+    """bench.NllAllReduce (configs[2]'s exchange, bucketed): every batch's row
+    is handed to exactly one all-reduce, after the kernel wrote it and before
+    the row is written again, for the synchronous and the overlapped forms --
+    checked with a recording stand-in for torch.distributed.all_reduce."""
+    import torch
+
+    class FakeRunner:
+        def __init__(self):
+            self.term_bufs = torch.zeros(2, bench.NLL_BUCKET, 3)
+            self.i = 0
+
+        def step(self):  # as bench.Runner.step: pick the row, then count the batch
+            self.terms = self.term_bufs[(self.i // bench.NLL_BUCKET) % 2,
+                                        self.i % bench.NLL_BUCKET]
+            self.terms.fill_(float(self.i))
+            self.i += 1
+
+    class Work:
+        def __init__(self, log, vals):
+            self.log, self.vals = log, vals
+
+        def wait(self):
+            self.log.append(("wait", self.vals))
+
+    for overlap in (False, True):
+        for steps in (1, 7, bench.NLL_BUCKET, 2 * bench.NLL_BUCKET + 3, 5 * bench.NLL_BUCKET):
+            log, reduced = [], []
+
+            def fake_all_reduce(t, async_op=False):
+                vals = tuple(int(v) for v in t[:, 0].tolist())
+                reduced.extend(vals)
+                log.append(("reduce", vals))
+                return Work(log, vals) if async_op else None
+
+            monkeypatch.setattr(bench.dist, "all_reduce", fake_all_reduce)
+            r = FakeRunner()
+            coll = bench.NllAllReduce(r, overlap=overlap)
+            for _ in range(steps):
+                r.step()
+                coll()
+            coll.drain()
+            assert sorted(reduced) == list(range(steps)), (overlap, steps)
+            if overlap:  # a bucket is waited for before its rows are written again
+                for k, (what, vals) in enumerate(log):
+                    if what == "reduce" and vals and vals[0] + 2 * bench.NLL_BUCKET < steps:
+                        assert ("wait", vals) in log[k + 1:], (steps, vals)
