@@ -1408,6 +1408,9 @@ struct Plan16 {
   int64_t tape, tbits, zst, ld, gld, g0, gbuf, seed, part, total, nkb, rows_kb, nseed;
 };
 constexpr double kTapeMaxBytes = 96.0 * (1ull << 30);  // beyond: the layer-at-a-time path
+#ifndef CNF_WDWG_NKB
+#define CNF_WDWG_NKB 256
+#endif
 
 bool plan16(const Shape& s, int64_t B, WTrain16Layout* lay, Plan16* p) {
   if (!wide16_train_ok(s) || wide16_train_layout(s, lay) != CNF_OK) return false;
@@ -1430,7 +1433,11 @@ bool plan16(const Shape& s, int64_t B, WTrain16Layout* lay, Plan16* p) {
   p->gbuf = take((int64_t)s.L * Bp * lay->GW);
   p->nseed = std::min<int64_t>(4096, (Bn + 15) / 16);  // k_wseed's blocks (generic seeds)
   p->seed = take(std::max<int64_t>(p->nseed, wide16_blocks(Bn)) * 4);  // or one record per wave
-  int64_t rows = (Bn + 255) / 256;
+  // k_wdw16g's row blocks: CNF_WDWG_NKB of them (each one record of dW
+  // partials that the fixed-order reduction reads back).  At cfg4 (2^18 rows)
+  // 256 measured 255 us per layer; 128 / 171 / 512 blocks 300 / 293 / 278 us
+  // (fewer blocks: a ragged last round of the 2-per-CU grid; more: partials)
+  int64_t rows = (Bn + CNF_WDWG_NKB - 1) / CNF_WDWG_NKB;
   rows = std::max<int64_t>(256, (rows + 31) / 32 * 32);
   p->rows_kb = rows;
   p->nkb = (Bn + rows - 1) / rows;
