@@ -675,6 +675,11 @@ __device__ __forceinline__ void wdwg_chunks(const DwJob& j, float* sm, int w, in
 #ifndef CNF_WDWG_RR
 #define CNF_WDWG_RR 1
 #endif
+// A/B timing only (wrong results): 1 = no MFMAs, 2 = no operand DMA (the
+// MFMAs run on whatever the LDS stages hold)
+#ifndef CNF_WDWG_KO
+#define CNF_WDWG_KO 0
+#endif
 template <int NTG, int NTH, int W>
 __device__ __forceinline__ void wdwg_rr(const DwJob& j, const DwArgs& da, float* sm, int lane,
                                         int64_t r0, int nch) {
@@ -686,6 +691,7 @@ __device__ __forceinline__ void wdwg_rr(const DwJob& j, const DwArgs& da, float*
 #pragma unroll
   for (int m = 0; m < NP; ++m) acc[m] = f4{};
   auto dma = [&](int c, int stg) {
+    if (CNF_WDWG_KO == 2) return;
     const float* gsrc = j.G + ((r0 >> 5) + c) * 32 * ldg;
     const float* hsrc = j.H + ((r0 >> 5) + c) * 32 * ldh;
     float* dst = sm + stg * TPC * 512;
@@ -714,7 +720,10 @@ __device__ __forceinline__ void wdwg_rr(const DwJob& j, const DwArgs& da, float*
 #pragma unroll
       for (int m = 0; m < NP; ++m) {
         const int p = W + 4 * m;
-        acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[p / NTH], b[p % NTH], acc[m], 0, 0, 0);
+        if (CNF_WDWG_KO == 1)
+          acc[m][0] += a[p / NTH] * b[p % NTH];
+        else
+          acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[p / NTH], b[p % NTH], acc[m], 0, 0, 0);
       }
     }
   }
