@@ -9,6 +9,10 @@
 
 #include "cnf_valu_common.h"
 
+#ifndef CNF_VALU_NT_STORE
+#define CNF_VALU_NT_STORE 1  // A/B: 0 = default-policy 16-B tile stores
+#endif
+
 namespace cnf {
 namespace valu {
 
@@ -43,9 +47,20 @@ __device__ __forceinline__ void tile_store(float* __restrict__ dst, const float*
   int done = 0;
   if (vec) {
     const int n4 = n >> 2;
-    float4* d4 = reinterpret_cast<float4*>(dst);
     const float4* s4 = reinterpret_cast<const float4*>(sm);
+#if CNF_VALU_NT_STORE
+    // streaming stores: the rows are written once and never re-read here
+    // (k_sgpr's whole-line nt stores measured the same way)
+    typedef float nt4 __attribute__((ext_vector_type(4)));
+    nt4* d4 = reinterpret_cast<nt4*>(dst);
+    for (int i = tid; i < n4; i += ROWS) {
+      const float4 q = s4[i];
+      __builtin_nontemporal_store(nt4{q.x, q.y, q.z, q.w}, d4 + i);
+    }
+#else
+    float4* d4 = reinterpret_cast<float4*>(dst);
     for (int i = tid; i < n4; i += ROWS) d4[i] = s4[i];
+#endif
     done = n4 << 2;
   }
   for (int i = done + tid; i < n; i += ROWS) dst[i] = sm[i];

@@ -5,7 +5,7 @@ pre-built launches (the shipped build's prepared blob: the builds must share
 cnf_prepare's layout) are timed build after build, round after round, so
 clock drift and box-to-box spread fall on every build alike.  Prints one JSON
 line per (mode, B): the median and min per-launch time of each build.
-usage: ab_interleave.py [modes=loss,forward] [Bs=1048576,8388608] [rounds=9]"""
+usage: ab_interleave.py [modes=loss,forward (also inverse, all: every layer's z)] [Bs=1048576,8388608] [rounds=9]"""
 import ctypes
 import glob
 import json
@@ -36,7 +36,8 @@ for mode in modes:
     for B in Bs:
         wl = "cfg5" if mode == "inverse" else "cfg2"
         w = dict(bench.WORKLOADS[wl], B=B)
-        r = bench.Runner(w, dev, 1.0e9, mode="loss" if mode == "loss" else "forward")
+        r = bench.Runner(w, dev, 1.0e9, all_outputs=(mode == "all"),
+                         mode="loss" if mode == "loss" else "forward")
         launches = max(24, (160 << 20) // B)
         r.settle(0.5)
         times = {k: [] for k in libs}
