@@ -12,6 +12,9 @@
 #ifndef CNF_VALU_NT_STORE
 #define CNF_VALU_NT_STORE 1  // A/B: 0 = default-policy 16-B tile stores
 #endif
+#ifndef CNF_VALU_NT_LOAD
+#define CNF_VALU_NT_LOAD 0  // A/B: streaming 16-B tile loads (every-layer pass 59.6 -> 65.1 us)
+#endif
 
 namespace cnf {
 namespace valu {
@@ -32,9 +35,18 @@ __device__ __forceinline__ void tile_load(float* __restrict__ sm, const float* _
   int done = 0;
   if (vec) {
     const int n4 = n >> 2;
-    const float4* s4 = reinterpret_cast<const float4*>(src);
     float4* d4 = reinterpret_cast<float4*>(sm);
+#if CNF_VALU_NT_LOAD
+    typedef float nt4 __attribute__((ext_vector_type(4)));
+    const nt4* s4 = reinterpret_cast<const nt4*>(src);
+    for (int i = tid; i < n4; i += ROWS) {
+      const nt4 q = __builtin_nontemporal_load(s4 + i);
+      d4[i] = float4{q.x, q.y, q.z, q.w};
+    }
+#else
+    const float4* s4 = reinterpret_cast<const float4*>(src);
     for (int i = tid; i < n4; i += ROWS) d4[i] = s4[i];
+#endif
     done = n4 << 2;
   }
   for (int i = done + tid; i < n; i += ROWS) sm[i] = src[i];
@@ -50,7 +62,7 @@ __device__ __forceinline__ void tile_store(float* __restrict__ dst, const float*
     const float4* s4 = reinterpret_cast<const float4*>(sm);
 #if CNF_VALU_NT_STORE
     // streaming stores: the rows are written once and never re-read here
-    // (k_sgpr's whole-line nt stores measured the same way)
+    // (every-layer pass at 2^20 rows 70.4 -> 57.4 us)
     typedef float nt4 __attribute__((ext_vector_type(4)));
     nt4* d4 = reinterpret_cast<nt4*>(dst);
     for (int i = tid; i < n4; i += ROWS) {
