@@ -668,7 +668,8 @@ int vjp_workspace(const Shape& s, int64_t B, size_t* bytes) {
     // the larger of the two variants (loss / generic) -- same grid rule
     const int64_t g = std::max(grid_v2(s, pick_v2(e2, s, true), B),
                                grid_v2(s, pick_v2(e2, s, false), B));
-    *bytes = v2_stash_offset(s, g) + (size_t)s.L * (B > 0 ? B : 1) * s.DT * 4;
+    // the stash: L x DT x (B rounded up to even) floats (k_vjp2's pair stores)
+    *bytes = v2_stash_offset(s, g) + (size_t)s.L * (((B > 0 ? B : 1) + 1) & ~(int64_t)1) * s.DT * 4;
     return CNF_OK;
   }
   const VEntry* e = find_entry(s);

@@ -326,6 +326,16 @@ __device__ __forceinline__ floatx4 wgrad_tile(float* st, const f2* G, const f2* 
   return acc;
 }
 
+// A/B: the x_T stash feature-major [L][DT][Bp] (whole-line stores) and
+// streaming (nt) stash traffic.  cfg2 step: row-major 0.1565-0.1577 ms,
+// feature-major 0.1581-0.1588, + nt stores 0.1647-0.1671, + nt loads too
+// 0.1643-0.1658 -- the stash is re-read one tile later and partly hits L2.
+#ifndef CNF_V2_STASH_FM
+#define CNF_V2_STASH_FM 0
+#endif
+#ifndef CNF_V2_STASH_NT
+#define CNF_V2_STASH_NT 0  // bit 0: streaming stash stores, bit 1: streaming stash loads
+#endif
 #ifndef CNF_V2_HLATE
 #define CNF_V2_HLATE 1  // the dW stack's 2^64 on h' applied once per wave (below)
 #endif
@@ -414,6 +424,7 @@ __global__ __launch_bounds__(64, CNF_V2_WPS) void k_vjp2(const float* __restrict
   constexpr int kStage = 32 * kV2SS;
   const int lane = threadIdx.x;
   const int64_t B = a.B;
+  const int64_t Bp = (B + 1) & ~(int64_t)1;  // stash rows per feature (8-B aligned pairs)
   const int L = a.L;
   const int ntiles = (int)((B + kV2TR - 1) / kV2TR);
   const f2 zero = splat(0.f, f2{});
@@ -472,8 +483,29 @@ __global__ __launch_bounds__(64, CNF_V2_WPS) void k_vjp2(const float* __restrict
 #pragma unroll
       for (int k = 0; k < DC; ++k) c[k] = v[R<D, O>(DT + k)];
       f2 h1[H1 ? H1 : 1], h2[H2 ? H2 : 1], t[DT], sv[DT];
-      {  // x_T of this layer, rows r, r+1: 2*DT contiguous floats as (row r,
-         // row r+1) pairs (8-B stores: the lane's slot starts 8-B aligned)
+      {  // x_T of this layer, rows r, r+1
+#if CNF_V2_STASH_FM
+        // feature-major [L][DT][Bp]: each 8-B store instruction writes 512
+        // contiguous bytes (whole lines), streamed past L2 (STASH_NT bit 0)
+        float* sp = a.stash + (int64_t)l * DT * Bp + r;
+        if (full) {
+#pragma unroll
+          for (int j = 0; j < DT; ++j) {
+            if (CNF_V2_STASH_NT & 1)
+              __builtin_nontemporal_store(v[R<D, O>(j)], reinterpret_cast<f2*>(sp + j * Bp));
+            else
+              *reinterpret_cast<f2*>(sp + j * Bp) = v[R<D, O>(j)];
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < DT; ++j) {
+            if (nr > 0) sp[j * Bp] = v[R<D, O>(j)].x;
+            if (nr > 1) sp[j * Bp + 1] = v[R<D, O>(j)].y;
+          }
+        }
+#else
+        // row-major [L][B][DT]: 2*DT contiguous floats as (row r, row r+1)
+        // pairs (8-B stores: the lane's slot starts 8-B aligned)
         float* sp = a.stash + ((int64_t)l * B + r) * DT;
         if (full) {
 #pragma unroll
@@ -485,6 +517,7 @@ __global__ __launch_bounds__(64, CNF_V2_WPS) void k_vjp2(const float* __restrict
             if (nr > 1) sp[2 * j + 1] = v[R<D, O>(j)].y;
           }
         }
+#endif
       }
       const float* ws = Wsp + (int64_t)l * LF;
       vnet_fwd_sp<S, NC>(ws + (NETS == 2 ? S::NF : 0), c, h1, h2, t);
@@ -696,6 +729,22 @@ __global__ __launch_bounds__(64, CNF_V2_WPS) void k_vjp2(const float* __restrict
       for (int j = 0; j < DT; ++j) gT[j] = g[R<D, Oi>(j)];
       f2 xT[DT];
       {
+#if CNF_V2_STASH_FM
+        const float* sp = a.stash + (int64_t)l * DT * Bp + r;
+        if (full) {
+#pragma unroll
+          for (int j = 0; j < DT; ++j) {
+            if (CNF_V2_STASH_NT & 2)
+              xT[j] = __builtin_nontemporal_load(reinterpret_cast<const f2*>(sp + j * Bp));
+            else
+              xT[j] = *reinterpret_cast<const f2*>(sp + j * Bp);
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < DT; ++j)
+            xT[j] = f2{nr > 0 ? sp[j * Bp] : 0.f, nr > 1 ? sp[j * Bp + 1] : 0.f};
+        }
+#else
         const float* sp = a.stash + ((int64_t)l * B + r) * DT;
         if (full) {
 #pragma unroll
@@ -705,6 +754,7 @@ __global__ __launch_bounds__(64, CNF_V2_WPS) void k_vjp2(const float* __restrict
           for (int j = 0; j < DT; ++j)
             xT[j] = f2{nr > 0 ? sp[2 * j] : 0.f, nr > 1 ? sp[2 * j + 1] : 0.f};
         }
+#endif
       }
       // recompute on the scaled weights: th / sh are 2^-64 h (relu' reads
       // their sign; the weight-gradient stack H takes 2^64 times them)
