@@ -6,11 +6,15 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 #include "cnf_valu_common.h"
 
 #ifndef CNF_VALU_NT_STORE
 #define CNF_VALU_NT_STORE 1  // A/B: 0 = default-policy 16-B tile stores
+#endif
+#ifndef CNF_DPP_SUM
+#define CNF_DPP_SUM 1  // block_sum3's wave sums by DPP (0: __shfl_xor butterfly)
 #endif
 #ifndef CNF_VALU_NT_LOAD
 #define CNF_VALU_NT_LOAD 0  // A/B: streaming 16-B tile loads (every-layer pass 59.6 -> 65.1 us)
@@ -226,8 +230,33 @@ __device__ __forceinline__ void tile_loss(const T* v, T ld, const int* y, int ki
 // partials in block order with one small follow-up launch (reduce_partials),
 // so the fused eval stays deterministic without any block waiting on a
 // device-scope hand-off.
+// Wave sum into lane 63 by DPP (row_shr 1/2/4/8 inside each 16-lane row,
+// then row_bcast 15 / 31 across rows): VALU ops with a few cycles of latency
+// each, where the xor butterfly's __shfl_xor is six dependent ds_bpermute
+// round trips through LDS.  Only lane 63's result is meaningful.
+__device__ __forceinline__ float wave_sum_dpp63(float v) {
+  auto dpp = [](float x, auto ctl) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+        0, __builtin_bit_cast(int, x), decltype(ctl)::value, 0xf, 0xf, false));
+  };
+  v += dpp(v, std::integral_constant<int, 0x111>{});  // row_shr:1
+  v += dpp(v, std::integral_constant<int, 0x112>{});  // row_shr:2
+  v += dpp(v, std::integral_constant<int, 0x114>{});  // row_shr:4
+  v += dpp(v, std::integral_constant<int, 0x118>{});  // row_shr:8
+  v += dpp(v, std::integral_constant<int, 0x142>{});  // row_bcast:15
+  v += dpp(v, std::integral_constant<int, 0x143>{});  // row_bcast:31
+  return v;
+}
+
 template <int ROWS>
 __device__ __forceinline__ void block_sum3(float a, float b, float c, float* sm, float* part) {
+#if CNF_DPP_SUM
+  a = wave_sum_dpp63(a);
+  b = wave_sum_dpp63(b);
+  c = wave_sum_dpp63(c);
+  const int tid = threadIdx.x, w = tid >> 6;
+  constexpr int kLead = 63;  // the lane holding the wave's sums
+#else
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) {
     a += __shfl_xor(a, off);
@@ -235,8 +264,10 @@ __device__ __forceinline__ void block_sum3(float a, float b, float c, float* sm,
     c += __shfl_xor(c, off);
   }
   const int tid = threadIdx.x, w = tid >> 6;
+  constexpr int kLead = 0;
+#endif
   lds_barrier();
-  if ((tid & 63) == 0) {
+  if ((tid & 63) == kLead) {
     sm[4 * w] = a;
     sm[4 * w + 1] = b;
     sm[4 * w + 2] = c;
@@ -292,13 +323,21 @@ __device__ __forceinline__ void reduce_rows4_block(const float4* __restrict__ pa
       s2 += v[k].z;
     }
   }
+#if CNF_DPP_SUM
+  s0 = wave_sum_dpp63(s0);
+  s1 = wave_sum_dpp63(s1);
+  s2 = wave_sum_dpp63(s2);
+  constexpr int kLead = 63;
+#else
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) {
     s0 += __shfl_xor(s0, off);
     s1 += __shfl_xor(s1, off);
     s2 += __shfl_xor(s2, off);
   }
-  if ((t & 63) == 0) {
+  constexpr int kLead = 0;
+#endif
+  if ((t & 63) == kLead) {
     red[t >> 6][0] = s0;
     red[t >> 6][1] = s1;
     red[t >> 6][2] = s2;
