@@ -883,14 +883,11 @@ __global__ __launch_bounds__(64, CNF_V2_WPS) void k_vjp2(const float* __restrict
       }
     });
   }
-  if constexpr (LOSS) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-      lt0 += __shfl_xor(lt0, off);
-      lt1 += __shfl_xor(lt1, off);
-      lt2 += __shfl_xor(lt2, off);
-    }
-    if (lane == 0) {
+  if constexpr (LOSS) {  // the wave's loss sums (DPP, into lane 63: cnf_valu_io.h)
+    lt0 = wave_sum_dpp63(lt0);
+    lt1 = wave_sum_dpp63(lt1);
+    lt2 = wave_sum_dpp63(lt2);
+    if (lane == 63) {
       out[P] = lt0;
       out[P + 1] = lt1;
       out[P + 2] = lt2;
