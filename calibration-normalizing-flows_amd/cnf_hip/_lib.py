@@ -30,7 +30,7 @@ EXPORTS = (
     "cnf_param_count", "cnf_param_tensor_count", "cnf_prepared_bytes", "cnf_prepare",
     "cnf_forward", "cnf_inverse", "cnf_forward_loss_workspace_bytes", "cnf_forward_loss",
     "cnf_predict", "cnf_vjp_workspace_bytes", "cnf_vjp", "cnf_loss_vjp", "cnf_adam_step",
-    "cnf_adam_step_sched",
+    "cnf_adam_step_sched", "cnf_adam_step_guarded",
     "cnf_vjp_inverse_workspace_bytes", "cnf_vjp_inverse", "cnf_guard_nonfinite",
     "cnf_kernel_name", "cnf_strerror", "cnf_last_hip_error", "cnf_abi_version",
 )
@@ -96,6 +96,8 @@ def _bind(lib):
                                          P]),
         "cnf_adam_step_sched": (ctypes.c_int, [D, ctypes.POINTER(P), P, P, P, P, DB, DB, DB, DB,
                                                P]),
+        "cnf_adam_step_guarded": (ctypes.c_int, [D, ctypes.POINTER(P), P, P, P, I64, DB, P, DB,
+                                                 DB, DB, DB, P, P]),
         "cnf_guard_nonfinite": (ctypes.c_int, [P, I64, P, P]),
         "cnf_kernel_name": (ctypes.c_char_p, [D]),
         "cnf_strerror": (ctypes.c_char_p, [ctypes.c_int]),

@@ -141,7 +141,10 @@ class StackAdam:
             torch.autograd.graph.increment_version(p)
         stats["adam"] = stats.get("adam", 0) + 1
 
-    def step(self, flat_grads):
+    def step(self, flat_grads, skip=None):
+        """One step.  skip: a device int32 flag (NonFiniteGuard.flag) read by
+        the kernel: non-zero leaves the parameters and moments untouched
+        (cnf_adam_step_guarded), with no host sync."""
         ps, dev = self._ensure_state()
         for p in ps:
             if not p.is_contiguous():
@@ -149,12 +152,23 @@ class StackAdam:
         self.t += 1
         arr = (ctypes.c_void_p * len(ps))(*[p.data_ptr() for p in ps])
         lib = _lib.lib()
-        st = lib.cnf_adam_step(ctypes.byref(self.stack.desc), arr, _ptr(flat_grads), _ptr(self._m),
-                               _ptr(self._v), ctypes.c_int64(self.t), ctypes.c_double(self.lr),
-                               ctypes.c_double(self.betas[0]), ctypes.c_double(self.betas[1]),
-                               ctypes.c_double(self.eps), ctypes.c_double(self.weight_decay),
-                               _stream(dev))
-        _lib.check("cnf_adam_step", st)
+        if skip is not None:
+            if skip.dtype != torch.int32 or skip.device != dev:
+                raise ValueError("StackAdam.step: skip must be a device int32 flag on %s" % dev)
+            st = lib.cnf_adam_step_guarded(
+                ctypes.byref(self.stack.desc), arr, _ptr(flat_grads), _ptr(self._m),
+                _ptr(self._v), ctypes.c_int64(self.t), ctypes.c_double(self.lr), None,
+                ctypes.c_double(self.betas[0]), ctypes.c_double(self.betas[1]),
+                ctypes.c_double(self.eps), ctypes.c_double(self.weight_decay), _ptr(skip),
+                _stream(dev))
+            _lib.check("cnf_adam_step_guarded", st)
+        else:
+            st = lib.cnf_adam_step(ctypes.byref(self.stack.desc), arr, _ptr(flat_grads),
+                                   _ptr(self._m), _ptr(self._v), ctypes.c_int64(self.t),
+                                   ctypes.c_double(self.lr), ctypes.c_double(self.betas[0]),
+                                   ctypes.c_double(self.betas[1]), ctypes.c_double(self.eps),
+                                   ctypes.c_double(self.weight_decay), _stream(dev))
+            _lib.check("cnf_adam_step", st)
         # the kernel wrote the parameters behind autograd's back: bump their
         # version counters, so every prepared-weight cache keyed on them (this
         # stack's and any other binding's) rebuilds

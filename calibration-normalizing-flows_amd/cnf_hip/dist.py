@@ -93,7 +93,9 @@ class ShardedFlowTrainer:
         # nan_guard: every native step also ORs the non-finite state of the
         # reduced [grads | loss terms] buffer into self.guard.flag (device int,
         # no host sync; the reference aborts its loop on NaN predictions,
-        # run_experiment3D.py:129-131 -- read self.guard.tripped() when wanted)
+        # run_experiment3D.py:129-131 -- read self.guard.tripped() when wanted),
+        # and the step's Adam update is skipped on the device when the flag is
+        # set, so the weights and moments stay at the last finite step
         self.nan_guard = nan_guard
         self.guard = None
         self.params = list(_coupling_params(flow))
@@ -138,7 +140,10 @@ class ShardedFlowTrainer:
                     self._adam.store_into(self.optimizer)
                     self._adam = None
                 self._set_grads(buf[:P])
-                self.optimizer.step()
+                # a torch optimizer cannot read the device flag: with the guard
+                # on, the host checks it (one sync) and skips a tripped step
+                if not (self.nan_guard and self.guard.tripped()):
+                    self.optimizer.step()
                 return buf[P:]
             if self._adam is None or self._adam.stack is not stack:
                 if self._adam is not None:
@@ -149,7 +154,10 @@ class ShardedFlowTrainer:
             # schedulers may move lr, betas (OneCycleLR / CyclicLR momentum
             # cycling), eps or weight decay between steps: read all of them
             self._adam.set_hparams(hp)
-            self._adam.step(buf[:P])
+            # guarded: a step whose reduced gradient or sums are non-finite
+            # updates nothing (the reference breaks out before opt.step(),
+            # run_experiment3D.py:129-133, keeping the last finite weights)
+            self._adam.step(buf[:P], skip=self.guard.flag if self.nan_guard else None)
             return buf[P:]
         grads, terms = local_loss_and_grads(self.flow, x, y, 1.0 / global_batch, kind, det)
         buf = torch.cat([grads, terms])

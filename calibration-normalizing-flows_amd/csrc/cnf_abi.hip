@@ -154,6 +154,7 @@ int cnf_prepared_bytes(const cnf_desc* desc, size_t* bytes) {
 }
 
 int cnf_prepare(const cnf_desc* desc, const float* const* params, void* prepared, void* stream) {
+  CNF_RANGE("cnf_prepare");
   Shape s;
   int st = derive_shape(desc, &s);
   if (st != CNF_OK) return st;
@@ -178,11 +179,13 @@ static int run(const cnf_desc* desc, const void* prepared, const float* in, floa
 
 int cnf_forward(const cnf_desc* desc, const void* prepared, const float* x, float* z,
                 float* logdet, float* z_all, int64_t B, void* stream) {
+  CNF_RANGE("cnf_forward");
   return run(desc, prepared, x, z, logdet, z_all, B, stream, false);
 }
 
 int cnf_inverse(const cnf_desc* desc, const void* prepared, const float* z, float* x,
                 float* logdet, float* x_all, int64_t B, void* stream) {
+  CNF_RANGE("cnf_inverse");
   return run(desc, prepared, z, x, logdet, x_all, B, stream, true);
 }
 
@@ -203,6 +206,7 @@ int cnf_forward_loss(const cnf_desc* desc, const void* prepared, const float* x,
                      const int64_t* y, int32_t loss_kind, float det, float* z, float* logdet,
                      float* loss_terms, int64_t B, void* workspace, size_t workspace_bytes,
                      void* stream) {
+  CNF_RANGE("cnf_forward_loss");
   Shape s;
   int st = derive_shape(desc, &s);
   if (st != CNF_OK) return st;
@@ -238,6 +242,7 @@ int cnf_forward_loss(const cnf_desc* desc, const void* prepared, const float* x,
 
 int cnf_predict(const cnf_desc* desc, const void* prepared, const float* x,
                 const float* log_priors, float* probs, float* logdet, int64_t B, void* stream) {
+  CNF_RANGE("cnf_predict");
   Shape s;
   int st = derive_shape(desc, &s);
   if (st != CNF_OK) return st;
@@ -267,6 +272,7 @@ int cnf_vjp_workspace_bytes(const cnf_desc* desc, int64_t B, size_t* bytes) {
 int cnf_vjp(const cnf_desc* desc, const void* prepared, const float* x, const float* gz,
             const float* gz_all, const float* gld, float* grads, float* dx, int64_t B,
             void* workspace, size_t workspace_bytes, void* stream) {
+  CNF_RANGE("cnf_vjp");
   Shape s;
   int st = derive_shape(desc, &s);
   if (st != CNF_OK) return st;
@@ -279,6 +285,7 @@ int cnf_vjp(const cnf_desc* desc, const void* prepared, const float* x, const fl
 int cnf_loss_vjp(const cnf_desc* desc, const void* prepared, const float* x, const int64_t* y,
                  int32_t loss_kind, float det, float grad_scale, float* loss_terms, float* grads,
                  float* dx, int64_t B, void* workspace, size_t workspace_bytes, void* stream) {
+  CNF_RANGE("cnf_loss_vjp");
   Shape s;
   int st = derive_shape(desc, &s);
   if (st != CNF_OK) return st;
@@ -301,6 +308,7 @@ int cnf_vjp_inverse_workspace_bytes(const cnf_desc* desc, int64_t B, size_t* byt
 int cnf_vjp_inverse(const cnf_desc* desc, const void* prepared, const float* z, const float* gx,
                     const float* gx_all, const float* gld, float* grads, float* dz, int64_t B,
                     void* workspace, size_t workspace_bytes, void* stream) {
+  CNF_RANGE("cnf_vjp_inverse");
   Shape s;
   int st = derive_shape(desc, &s);
   if (st != CNF_OK) return st;

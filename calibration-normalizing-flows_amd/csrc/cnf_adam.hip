@@ -35,9 +35,14 @@ struct AdamArgs {
   // device {step_size, bc2_sqrt} (cnf_adam_step_sched: graph-captured steps,
   // whose kernel arguments are fixed at capture); nullptr: the two above
   const float* sched;
+  // device int32 flag (cnf_adam_step_guarded): non-zero skips the whole update,
+  // so a step whose gradient tripped the non-finite guard leaves the
+  // parameters and moments at the last finite step; nullptr: always update
+  const int32_t* skip;
 };
 
 __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
+  if (a.skip && __builtin_amdgcn_readfirstlane(*a.skip) != 0) return;
   const int ti = blockIdx.y;
   const int64_t o0 = a.off[ti], n = a.off[ti + 1] - o0;
   float* __restrict__ p = a.p[ti];
@@ -69,7 +74,7 @@ namespace {
 
 int adam_launch(const cnf_desc* desc, float* const* params, const float* grads, float* exp_avg,
                 float* exp_avg_sq, int64_t step, double lr, double beta1, double beta2, double eps,
-                double weight_decay, const float* sched, void* stream) {
+                double weight_decay, const float* sched, const int32_t* skip, void* stream) {
   Shape s;
   int st = derive_shape(desc, &s);
   if (st != CNF_OK) return st;
@@ -81,6 +86,7 @@ int adam_launch(const cnf_desc* desc, float* const* params, const float* grads, 
   const double bc2 = sched ? 1.0 : 1.0 - std::pow(beta2, (double)step);
   AdamArgs a{};
   a.sched = sched;
+  a.skip = skip;
   a.g = grads;
   a.m = exp_avg;
   a.v = exp_avg_sq;
@@ -136,15 +142,28 @@ extern "C" int cnf_adam_step(const cnf_desc* desc, float* const* params, const f
                              float* exp_avg, float* exp_avg_sq, int64_t step, double lr,
                              double beta1, double beta2, double eps, double weight_decay,
                              void* stream) {
+  CNF_RANGE("cnf_adam_step");
   return adam_launch(desc, params, grads, exp_avg, exp_avg_sq, step, lr, beta1, beta2, eps,
-                     weight_decay, nullptr, stream);
+                     weight_decay, nullptr, nullptr, stream);
 }
 
 extern "C" int cnf_adam_step_sched(const cnf_desc* desc, float* const* params,
                                    const float* grads, float* exp_avg, float* exp_avg_sq,
                                    const float* sched, double beta1, double beta2, double eps,
                                    double weight_decay, void* stream) {
+  CNF_RANGE("cnf_adam_step_sched");
   if (!sched) return CNF_ERR_NULL;
   return adam_launch(desc, params, grads, exp_avg, exp_avg_sq, 0, 0.0, beta1, beta2, eps,
-                     weight_decay, sched, stream);
+                     weight_decay, sched, nullptr, stream);
+}
+
+extern "C" int cnf_adam_step_guarded(const cnf_desc* desc, float* const* params,
+                                     const float* grads, float* exp_avg, float* exp_avg_sq,
+                                     int64_t step, double lr, const float* sched, double beta1,
+                                     double beta2, double eps, double weight_decay,
+                                     const int32_t* skip_flag, void* stream) {
+  CNF_RANGE("cnf_adam_step_guarded");
+  if (!skip_flag) return CNF_ERR_NULL;
+  return adam_launch(desc, params, grads, exp_avg, exp_avg_sq, step, lr, beta1, beta2, eps,
+                     weight_decay, sched, skip_flag, stream);
 }

@@ -53,6 +53,7 @@ __global__ __launch_bounds__(256) void k_guard(const float* __restrict__ a, int6
 
 extern "C" int cnf_guard_nonfinite(const float* data, int64_t n, int32_t* flag, void* stream) {
   using namespace cnf;
+  CNF_RANGE("cnf_guard_nonfinite");
   if (n < 0) return CNF_ERR_BATCH;
   if (!flag || (n > 0 && !data)) return CNF_ERR_NULL;
   if ((reinterpret_cast<uintptr_t>(data) & 3) || (reinterpret_cast<uintptr_t>(flag) & 3))

@@ -9,6 +9,26 @@
 
 #include "cnf.h"
 
+// roctx ranges around every launching C-ABI entry point (SURVEY.md section 5,
+// tracing): compiled in only by `make roctx` (-DCNF_ROCTX, linked against
+// rocprofiler-sdk-roctx; never the shipped build, which reads no environment
+// and loads no tracer), so a `rocprofv3 --marker-trace --kernel-trace` run of
+// that build ties each cnf_* host call to the kernels it launched.
+#ifdef CNF_ROCTX
+#include <rocprofiler-sdk-roctx/roctx.h>
+namespace cnf {
+struct RoctxRange {
+  explicit RoctxRange(const char* name) { roctxRangePushA(name); }
+  ~RoctxRange() { roctxRangePop(); }
+};
+}  // namespace cnf
+#define CNF_RANGE(name) ::cnf::RoctxRange cnf_roctx_range_(name)
+#else
+#define CNF_RANGE(name) \
+  do {                  \
+  } while (0)
+#endif
+
 namespace cnf {
 
 constexpr int kMaxLin = CNF_MAX_HIDDEN + 1;  // Linear layers per conditioner MLP

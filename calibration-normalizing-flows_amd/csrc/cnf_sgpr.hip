@@ -42,10 +42,9 @@
 //     tile's rows are in registers by then, ds_write2_b32 per feature pair),
 //     and the wave stores the tile lane-linear with streaming 16-B stores, each
 //     instruction 1 KiB contiguous; the next tile's LDS-DMA is issued once the
-//     staged rows have been read back (kStage 1 below);
-//   * a persistent grid (CUs x resident blocks) walks the tiles wave by wave
-//     (priority schedules by tiles remaining were measured and lost:
-//     CNF_SGPR_PRIO, off).
+//     staged rows have been read back;
+//   * a persistent grid (CUs x resident blocks) walks the tiles wave by wave,
+//     the waves with more tiles left at higher priority (s_setprio).
 // Every variant is compile-time (mode, random_flip, every-layer stores), so
 // the hot loop has no data-dependent branches and no scratch.
 #include <hip/hip_runtime.h>
@@ -89,58 +88,21 @@ namespace {
 
 using namespace valu;
 
-#ifndef CNF_SGPR_KWAVES  // A/B: waves per block (the grid cap below stays in waves per SIMD)
-#define CNF_SGPR_KWAVES 4
-#endif
-constexpr int kWaves = CNF_SGPR_KWAVES;  // waves per block
+constexpr int kWaves = 4;  // waves per block
 
-// Output path of the full tiles (cnf_sgpr_common.h stage_pairs / store_tile):
-//   0  16-B stores straight from registers, deferred one tile (round 2);
-//   1  staged through the wave's LDS tile, stored lane-linear; the next
-//      tile's LDS-DMA is issued after the staged tile has been read back;
-//   2  staged through a second LDS tile per wave, stores deferred one tile,
-//      the next tile's DMA issued before the compute (twice the LDS).
-// (A fourth form -- the next tile's DMA issued right after this tile's rows
-// reach registers, outputs staged through a half-size buffer so five waves
-// still fit -- measured 1.5 us SLOWER per 2^20-row loss call and no faster at
-// 2^23: the wave's DMA wait is not what limits the kernel, VALU issue is.)
-#ifndef CNF_SGPR_STAGE
-#define CNF_SGPR_STAGE 1
-#endif
-constexpr int kStage = CNF_SGPR_STAGE;
-// Loss mode: the block-order sum of the per-block loss records by the
-// launch's last block (cnf_valu_io.h block_sum3_handoff) instead of a
-// one-block follow-up launch.
-#ifndef CNF_SGPR_FUSED_RED
-#define CNF_SGPR_FUSED_RED 0
-#endif
-constexpr bool kFusedRed = CNF_SGPR_FUSED_RED != 0;
-// Loss mode picks z[y] from the staged output tile (one LDS read per row);
-// A/B builds: -DCNF_SGPR_NO_GATHER=1 keeps the register select tree.
-#ifndef CNF_SGPR_NO_GATHER
-#define CNF_SGPR_NO_GATHER 0
-#endif
-
-
-
-// Row pairs per lane.  Two pairs (4 rows per lane) let each SGPR weight feed
-// two FMAs (half the scalar-load traffic per row), at 4 waves per SIMD instead
-// of 5; measured on cfg2 it is no faster for the forward pass and 7-19 %
-// slower for the fused loss pass (register pressure), so one pair ships.
-// Every-layer outputs and random_flip stacks always use one pair.
-#ifndef CNF_SGPR_PAIRS
-#define CNF_SGPR_PAIRS 1
-#endif
+// One row pair per lane (two rows, one packed register per feature).  Two
+// pairs per lane (half the scalar-load traffic per row, 4 waves per SIMD) were
+// no faster for the forward pass and 7-19 % slower for the fused loss pass;
+// 8- and 12-wave blocks, a second LDS tile per wave (the next tile's DMA ahead
+// of the compute), 16-B stores straight from registers, 5 or 7 waves per SIMD,
+// priority schedules other than tiles-remaining and in-launch sums of the loss
+// records were measured and lost.
 template <bool ALL, bool PERM>
-constexpr int pairs_per_lane() { return (ALL || PERM) ? 1 : CNF_SGPR_PAIRS; }
-// register budget (resident waves per SIMD) for a lane of P pairs
-#ifndef CNF_SGPR_WPS  // A/B builds: -DCNF_SGPR_WPS=n for the unpermuted one-pair variants
-#define CNF_SGPR_WPS 6
-#endif
+constexpr int pairs_per_lane() { return 1; }
+// resident waves per SIMD (the register budget): 6, or 4 for random_flip
+// stacks (the permuted gathers)
 template <int MODE, bool ALL, bool PERM>
-constexpr int waves_per_simd() {
-  return pairs_per_lane<ALL, PERM>() == 2 ? 4 : (PERM || kStage == 2 ? 4 : CNF_SGPR_WPS);
-}
+constexpr int waves_per_simd() { return PERM ? 4 : 6; }
 
 enum Mode { kFwd = 0, kInv = 1, kLoss = 2, kPredict = 3 };
 
@@ -181,13 +143,8 @@ __device__ __forceinline__ void slin(const SW<NC>& w, X&& x, E&& emit, F&& befor
     for (int o = 0; o < NOUT; ++o)
 #pragma unroll
       for (int q = 0; q < P; ++q) {
-#ifdef CNF_AB_FMA_BUILTIN  // A/B: the compiler's broadcast (copies odd weights to a scratch pair)
-        if (RELU && k == NIN - 1) a[o][q] = fma_clamp(w[o * S + 1 + k], x(q, k), a[o][q]);
-        else a[o][q] = fmaT(w[o * S + 1 + k], x(q, k), a[o][q]);
-#else
         if (RELU && k == NIN - 1) a[o][q] = fma_ws_clamp(w, o * S + 1 + k, x(q, k), a[o][q]);
         else a[o][q] = fma_ws(w, o * S + 1 + k, x(q, k), a[o][q]);
-#endif
       }
 #pragma unroll
   for (int o = 0; o < NOUT; ++o) emit(o, a[o]);
@@ -279,11 +236,7 @@ __device__ __forceinline__ void sp_step(f2 (&v)[P][D], f2 (&ld)[P], SW<SP<D, H1,
       if constexpr (NETS == 1) {  // scale=False: s = 0, exp(0) = 1, log-det += 0
         x = INV ? x - a[p] : x + a[p];
       } else if constexpr (!INV) {
-#ifdef CNF_AB_NO_EXP  // A/B timing only (wrong results): a 4-cycle VALU op per exp
-        x = fmaV(x, a[p] + x, ac.t[p][j]);
-#else
         x = fmaV(x, exp2T(a[p]), ac.t[p][j]);
-#endif
         ld[p] += a[p];
       } else {
         x = (x - ac.t[p][j]) * exp2T(-a[p]);
@@ -337,8 +290,8 @@ __device__ __forceinline__ f2 pair_max(const f2* v) {
 // CE:  loss = -log_softmax(z)[y] - det * ld         run_experiment3D.py:107
 // z[y]: GATHER 1 reads it from the staged output tile (the lane's two rows at
 // tile[0..D) and tile[D..2D): one ds_read_b32 per row instead of a
-// ~30-instruction select tree); GATHER 2 takes the two values gathered by the
-// caller (tile[0], tile[1]); GATHER 0 selects from the registers (ragged tile).
+// ~30-instruction select tree); GATHER 0 selects from the registers (ragged
+// tile).
 template <int D, int GATHER>
 __device__ __forceinline__ void pair_loss(const f2* v, f2 ld, uint32_t lab2, int rows, int kind,
                                           float det, float& t0, float& t1, float& t2,
@@ -350,9 +303,6 @@ __device__ __forceinline__ void pair_loss(const f2* v, f2 ld, uint32_t lab2, int
   if constexpr (GATHER == 1) {  // issued first: the LDS reads overlap the max / sum-exp below
     zy[0] = tile[ok[0] ? (int)b0 : 0];
     zy[1] = tile[D + (ok[1] ? (int)b1 : 0)];
-  } else if constexpr (GATHER == 2) {  // gathered by the caller (kStage 3)
-    zy[0] = tile[0];
-    zy[1] = tile[1];
   }
   const f2 m = pair_max<D>(v);
   const f2 nm = m * splat(-kL2E, f2{});
@@ -447,8 +397,10 @@ struct KArgs {
   float* all;             // [L][B][D] every-layer outputs (ALL variants)
   const int64_t* y;       // labels (loss)
   float* part;            // per-block loss partials, 4 floats each (loss)
-  uint32_t* ctr;          // arrival counter of the in-launch block-order sum (loss)
-  float* terms;           // loss_terms[3] (loss, in-launch sum)
+  // three unused words: they keep the argument block of the measured build
+  // (the scalar loads of L / kind / det at these offsets; without them the
+  // compiler schedules every variant differently)
+  const void *reserved0, *reserved1, *reserved2;
   int L, kind;
   float det;
 };
@@ -491,7 +443,10 @@ __global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) v
     const int m = (int)(reinterpret_cast<uintptr_t>(q) & 15);
     return m == 0 ? 16 : ((m & 7) == 0 ? 8 : 4);
   };
-  const int al = a.out ? align_of(a.out) : 16;
+  // (no longer read: kept because this early look at a.out shapes the
+  // prologue's scalar-load schedule -- without it every variant compiles to a
+  // different instruction stream than the measured build)
+  [[maybe_unused]] const int al = a.out ? align_of(a.out) : 16;
   const int al_ld = a.ld ? align_of(a.ld) : 16;
   const bool y16 = MODE == kLoss && (reinterpret_cast<uintptr_t>(a.y) & 15) == 0;
   float lp[MODE == kPredict ? D : 1];
@@ -572,17 +527,11 @@ __global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) v
       const int r = nr - 2 * p;
       constexpr int G = decltype(gather)::value;
       pair_loss<D, G>(v[p], ld[p], lab >> (16 * p), r < 0 ? 0 : (r > 2 ? 2 : r), a.kind, a.det,
-                      lt0, lt1, lt2, tile + (G == 2 ? 2 : 2 * D) * p);
+                      lt0, lt1, lt2, tile + 2 * D * p);
     }
   };
 
-#ifdef CNF_AB_EMPTY  // A/B timing only: every wave exits at once (launch + drain floor)
-  if (B > 0) return;
-#endif
-#ifdef CNF_AB_VGPR80  // A/B: the forward variant forced to >= 80 VGPRs (dispatch-spread test)
-  if constexpr (MODE == kFwd) asm volatile("v_mov_b32 v79, 0" ::: "v79");
-#endif
-  // -------- full tiles: LDS-DMA in, deferred 16-B stores out --------
+  // -------- full tiles: LDS-DMA in, staged lane-linear stores out --------
   CNF_TR(0);
   CNF_TRC(0);
 #ifdef CNF_SGPR_TRACE
@@ -591,52 +540,20 @@ __global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) v
                             __builtin_amdgcn_s_getreg((31 << 11) | 4);  // XCC_ID, HW_ID
   int ntr = 0;
 #endif
-#ifndef CNF_SGPR_PRIO
-#define CNF_SGPR_PRIO 0
-#endif
-  // PRIO 3: the youngest waves own the extra tiles (tile walk from the last wave)
-  const int gwt = CNF_SGPR_PRIO == 3 ? nw - 1 - gw : gw;
-  if (CNF_SGPR_PRIO == 3) left = gwt < ntiles ? (ntiles - 1 - gwt) / nw + 1 : 0;
-  const int owned = left;
-  int t = gwt;
-#ifdef CNF_AB_STAGGER  // A/B: later resident blocks of a CU request their first tile later
-  {
-    const int slot = (int)(((int64_t)blockIdx.x * CNF_SGPR_GRID_WPS) / gridDim.x);
-    for (int i = 0; i < slot; ++i) __builtin_amdgcn_s_sleep(CNF_AB_STAGGER);
-  }
-#endif
-#ifdef CNF_AB_NO_MEM  // A/B timing only (wrong results): no input DMA, no label loads, no stores
-  constexpr bool kNoMem = true;
-  a.out = nullptr;
-  a.ld = nullptr;
-#else
-  constexpr bool kNoMem = false;
-#endif
-  if (!kNoMem && t < nfull) wave_dma<D, TR>(sm, in + (int64_t)t * TF, lane);
+  int t = gw;
+  if (t < nfull) wave_dma<D, TR>(sm, in + (int64_t)t * TF, lane);
+  // the wave with more tiles left goes first (VALU issue is arbitrated by
+  // priority, then age): the tail of a 2^20-row grid is 8 tiles on 6 waves
   auto set_prio = [&]() {
     --left;  // tiles after this one
-#ifndef CNF_AB_NO_PRIO
-    if constexpr (CNF_SGPR_PRIO == 0) {  // longest-remaining first
-      if (left >= 3) __builtin_amdgcn_s_setprio(3);
-      else if (left == 2) __builtin_amdgcn_s_setprio(2);
-      else if (left == 1) __builtin_amdgcn_s_setprio(1);
-      else __builtin_amdgcn_s_setprio(0);
-    } else if constexpr (CNF_SGPR_PRIO == 1) {  // every wave's first tile ahead of later ones
-      if (left + 1 == owned) __builtin_amdgcn_s_setprio(1);
-      else __builtin_amdgcn_s_setprio(0);
-    } else if constexpr (CNF_SGPR_PRIO == 2) {  // tiles with successors, then lone tiles, then last
-      if (left >= 1) __builtin_amdgcn_s_setprio(2);
-      else if (owned == 1) __builtin_amdgcn_s_setprio(1);
-      else __builtin_amdgcn_s_setprio(0);
-    }
-#endif
+    if (left >= 3) __builtin_amdgcn_s_setprio(3);
+    else if (left == 2) __builtin_amdgcn_s_setprio(2);
+    else if (left == 1) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
   };
-  [[maybe_unused]] float* stg = smem + (kWaves + wv) * TF;  // kStage 2: the output tile
-  f2 pz[kStage == 0 ? P : 1][D], pld[P];
-  int64_t prow = -1;  // first row of the lane's pending (not yet stored) outputs
   for (; t < nfull; t += nw) {
     set_prio();
-    if (!kNoMem) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA has landed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA has landed
     f2 v[P][D];
     if constexpr (P == 1) {  // rows are in registers (reversed for an odd stack)
       if (odd) read_pairs_wait<D, true>(sm, lane, v);
@@ -650,65 +567,29 @@ __global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) v
     if (ntr < 2) CNF_TR(1 + 2 * ntr);
 #endif
     const int64_t row0 = (int64_t)t * TR;
-    if (kStage != 1 && prow >= 0) {  // the previous tile's outputs, after this tile's reads
-      if constexpr (kStage == 0) {
-        if (a.out) store_rows<D, P>(a.out + prow * D, pz, 2 * P, al);
-      } else {
-        if (a.out) store_tile<TF>(a.out + (prow - 2 * P * lane) * D, stg, lane);
-      }
-      if (a.ld) store_lds<P>(a.ld + prow, pld, 2 * P, al_ld);
-    }
-    if (kStage != 1 && t + nw < nfull) wave_dma<D, TR>(sm, in + (int64_t)(t + nw) * TF, lane);
     uint32_t lab = 0;
-    if constexpr (MODE == kLoss)
-      if (!kNoMem) lab = load_labels<D, P>(a.y + row0 + 2 * P * lane, 2 * P, y16);
+    if constexpr (MODE == kLoss) lab = load_labels<D, P>(a.y + row0 + 2 * P * lane, 2 * P, y16);
     f2 ld[P];
     compute(v, ld, row0, 2 * P);
     if constexpr (MODE == kLoss) {
-      if constexpr (kStage == 1 && !CNF_SGPR_NO_GATHER) {
-        // staged first: the loss reads z[y] back from the tile
-        stage_pairs<D, P>(sm, lane, v);
-        loss(v, ld, lab, 2 * P, sm + 2 * P * D * lane, std::integral_constant<int, 1>{});
-      } else {
-        loss(v, ld, lab, 2 * P, sm, std::integral_constant<int, 0>{});
-      }
+      // staged first: the loss reads z[y] back from the tile
+      stage_pairs<D, P>(sm, lane, v);
+      loss(v, ld, lab, 2 * P, sm + 2 * P * D * lane, std::integral_constant<int, 1>{});
     }
 #ifdef CNF_SGPR_TRACE
     if (ntr < 2) CNF_TR(2 + 2 * ntr);
     CNF_TR(5);
     ++ntr;
 #endif
-    if constexpr (kStage == 1) {
-      // stage in the input tile (its rows are in registers), store lane-linear,
-      // then let the next tile's DMA in once the staged reads have completed
-      if (a.out) {
-        if (MODE != kLoss || CNF_SGPR_NO_GATHER) stage_pairs<D, P>(sm, lane, v);
-        store_tile<TF>(a.out + row0 * D, sm, lane);
-      }
-      if (a.ld) store_lds<P>(a.ld + row0 + 2 * P * lane, ld, 2 * P, al_ld);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (!kNoMem && t + nw < nfull) wave_dma<D, TR>(sm, in + (int64_t)(t + nw) * TF, lane);
-    } else {
-      if constexpr (kStage == 0) {
-#pragma unroll
-        for (int p = 0; p < P; ++p)
-#pragma unroll
-          for (int k = 0; k < D; ++k) pz[p][k] = v[p][k];
-      } else {
-        if (a.out) stage_pairs<D, P>(stg, lane, v);
-      }
-#pragma unroll
-      for (int p = 0; p < P; ++p) pld[p] = ld[p];
-      prow = row0 + 2 * P * lane;
+    // stage in the input tile (its rows are in registers), store lane-linear,
+    // then let the next tile's DMA in once the staged reads have completed
+    if (a.out) {
+      if (MODE != kLoss) stage_pairs<D, P>(sm, lane, v);
+      store_tile<TF>(a.out + row0 * D, sm, lane);
     }
-  }
-  if (kStage != 1 && prow >= 0) {
-    if constexpr (kStage == 0) {
-      if (a.out) store_rows<D, P>(a.out + prow * D, pz, 2 * P, al);
-    } else {
-      if (a.out) store_tile<TF>(a.out + (prow - 2 * P * lane) * D, stg, lane);
-    }
-    if (a.ld) store_lds<P>(a.ld + prow, pld, 2 * P, al_ld);
+    if (a.ld) store_lds<P>(a.ld + row0 + 2 * P * lane, ld, 2 * P, al_ld);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (t + nw < nfull) wave_dma<D, TR>(sm, in + (int64_t)(t + nw) * TF, lane);
   }
   // -------- the ragged last tile (B % TR rows): plain loads, masked stores --------
   if (t == nfull && nfull < ntiles) {
@@ -739,12 +620,7 @@ __global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) v
   }
   CNF_TRC(1);
   CNF_TR(6);
-  if constexpr (MODE == kLoss) {
-    if constexpr (kFusedRed)
-      block_sum3_handoff<kWaves * 64>(lt0, lt1, lt2, smem, a.part, a.ctr, (int)gridDim.x, a.terms);
-    else
-      block_sum3<kWaves * 64>(lt0, lt1, lt2, smem, a.part);
-  }
+  if constexpr (MODE == kLoss) block_sum3<kWaves * 64>(lt0, lt1, lt2, smem, a.part);
 }
 
 using KFn = void (*)(const float*, int64_t, const float*, const int32_t*, const int32_t*,
@@ -801,7 +677,7 @@ const SEntry* find(const Shape& s) {
 }
 
 size_t lds_bytes(const Shape& s, const KV& k) {
-  return (size_t)kWaves * k.tr * s.D * 4 * (kStage == 2 ? 2 : 1);
+  return (size_t)kWaves * k.tr * s.D * 4;
 }
 
 int resident_blocks(const KV& k, size_t lds) {
@@ -814,16 +690,14 @@ int resident_blocks(const KV& k, size_t lds) {
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k.fn, kWaves * 64, lds) != hipSuccess ||
       n < 1)
     n = 1;
-  // at most CNF_SGPR_GRID_WPS blocks per CU even where the occupancy query
+  // at most kGridWps blocks per CU even where the occupancy query
   // allows more: at 7 per CU (forward, 71 VGPRs) the last ~10 % of a 2^20-row
   // grid was not resident at launch and started ~18 us late (tools/sgpr_trace.py).
   // 6 (with the 6-wave register budget, 80 VGPRs, no scratch) measured 0.6-0.8 us
   // faster per 2^20-row loss / forward call than 5 (round 4, two interleaved
   // A/B passes); 7 spills the loss build
-#ifndef CNF_SGPR_GRID_WPS
-#define CNF_SGPR_GRID_WPS 6
-#endif
-  if (n > CNF_SGPR_GRID_WPS * 4 / kWaves) n = CNF_SGPR_GRID_WPS * 4 / kWaves;
+  constexpr int kGridWps = 6;
+  if (n > kGridWps * 4 / kWaves) n = kGridWps * 4 / kWaves;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
       cus < 1)
@@ -878,7 +752,7 @@ int sgpr_run(const Shape& s, const void* prepared, const float* in, float* out, 
   if (B == 0) return CNF_OK;
   if (B / 128 > 0x7fffffffLL) return CNF_ERR_UNSUPPORTED;
   // staged tile stores write whole 16-B words: a misaligned output view stays on k_valu
-  if (!io_ok(in, 16) || !io_ok(out, kStage ? 16 : 4) || !io_ok(all, 16) || !io_ok(ld, 4))
+  if (!io_ok(in, 16) || !io_ok(out, 16) || !io_ok(all, 16) || !io_ok(ld, 4))
     return CNF_ERR_UNSUPPORTED;
   const int mode = log_priors ? kPredict : (loss_ws ? kLoss : (inverse ? kInv : kFwd));
   const KV* k = pick(e, s, mode, all != nullptr);
@@ -889,35 +763,20 @@ int sgpr_run(const Shape& s, const void* prepared, const float* in, float* out, 
   const int32_t* flags = inv_q + s.L * s.D;
   const float* W = reinterpret_cast<const float*>(base + idx_bytes(s)) + s.sp_region;
   KArgs a{};
-#ifdef CNF_AB_NO_Z  // A/B timing only: outputs not written
-  out = nullptr;
-#endif
-#ifdef CNF_AB_NO_LD
-  ld = nullptr;
-#endif
   a.out = out;
   a.ld = ld;
   a.all = all;
   a.y = y;
   a.part = loss_ws ? loss_ws + 4 : nullptr;
-  a.ctr = reinterpret_cast<uint32_t*>(loss_ws);
-  a.terms = loss_terms;
   a.L = s.L;
   a.kind = kind;
   a.det = det;
   const int64_t nblk = grid_for(*k, s, B);
   hipLaunchKernelGGL(k->fn, dim3((unsigned)nblk), dim3(kWaves * 64), lds_bytes(s, *k), st, in, B,
                      W, inverse ? inv_q : fwd_q, flags, log_priors, a);
-  // the block-order sum of the loss records: a one-block follow-up launch.
-  // (A last-block hand-off inside k_sgpr -- agent-scope fence + counter per
-  // block -- measured 67.6 vs 35.6 us per 2^20-row call while z was written
-  // through L2: each block's release fence writes back its XCD's L2.  With
-  // the streaming z stores it ties (32.4 vs 32.3 us) and would add a
-  // zeroed-workspace contract, so the follow-up launch stays.)
-#ifndef CNF_AB_NO_REDUCE  // A/B timing only: the loss sums are not formed
-  if (mode == kLoss && !kFusedRed)
-    reduce_partials(loss_ws + 4, (int)nblk, 4, 0, nullptr, loss_terms, st);
-#endif
+  // the block-order sum of the loss records: a one-block follow-up launch
+  // (in-launch sums measured slower: cnf_valu_io.h reduce_rows4_block)
+  if (mode == kLoss) reduce_partials(loss_ws + 4, (int)nblk, 4, 0, nullptr, loss_terms, st);
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) {
     set_hip_error(err);

@@ -130,15 +130,13 @@ __device__ __forceinline__ void sissue(SW<NC>& r, const float* p) {
 
 // HBM -> LDS copy of one full wave tile (TR*D floats, 16-B aligned) by
 // LDS-DMA: one global_load_lds_dwordx4 moves 1 KiB, lane-linear.
-// CNF_SGPR_DMA_AUX: the loads' cache-policy bits (gfx950: 1 sc0, 2 nt, 16
-// sc1).  Streaming (nt) input: the cfg2 pass is held at the board's power cap
+// kDmaAux: the loads' cache-policy bits (gfx950: 1 sc0, 2 nt, 16 sc1).
+// Streaming (nt) input: the cfg2 pass is held at the board's power cap
 // (1.4 kW at 2^23 rows; tools/power_probe.py), and the nt DMA takes 8 % less
 // energy per row than the default policy -- 31.39 -> 30.24 us per 2^20-row
 // loss call, 192.8 -> 188.9 us at 2^23, outputs bitwise unchanged (round 5,
 // profiles/r05_ab_power.jsonl); sc1 nt measured the same as nt.
-#ifndef CNF_SGPR_DMA_AUX
-#define CNF_SGPR_DMA_AUX 2
-#endif
+constexpr int kDmaAux = 2;
 template <int D, int TR>
 __device__ __forceinline__ void wave_dma(float* sm, const float* __restrict__ src, int lane) {
   constexpr int N4 = TR * D / 4, NI = (N4 + 63) / 64;
@@ -147,7 +145,7 @@ __device__ __forceinline__ void wave_dma(float* sm, const float* __restrict__ sr
     if (N4 % 64 == 0 || i * 64 + lane < N4)
       __builtin_amdgcn_global_load_lds(src + (i * 64 + lane) * 4,
                                        (__attribute__((address_space(3))) void*)(sm + i * 256), 16,
-                                       0, CNF_SGPR_DMA_AUX);
+                                       0, kDmaAux);
   }
 }
 
@@ -271,13 +269,12 @@ __device__ __forceinline__ void store_tile(float* __restrict__ dst, const float*
 #pragma unroll
   for (int i = 0; i < NI; ++i)
     if (N4 % 64 == 0 || i * 64 + lane < N4) {
-#ifndef CNF_SGPR_NO_NT  // streaming stores: whole lines that need no write-back from L2 at kernel end
+      // streaming (nt) stores.  Write-through (sc1, sc0 sc1, sc1 nt) measured
+      // 28-49 % slower per 2^20-row call (round 6): the stores then wait on
+      // the fabric instead of draining from L2
       using v4 = __attribute__((ext_vector_type(4))) float;
       __builtin_nontemporal_store(v4{q[i].x, q[i].y, q[i].z, q[i].w},
                                   reinterpret_cast<v4*>(dst) + i * 64 + lane);
-#else
-      reinterpret_cast<float4*>(dst)[i * 64 + lane] = q[i];
-#endif
     }
 }
 
@@ -318,11 +315,7 @@ __device__ __forceinline__ void store_lds(float* __restrict__ dst, const f2 (&ld
   } else if (rows == 2 * P && al >= 8) {
 #pragma unroll
     for (int p = 0; p < P; ++p) {
-#ifdef CNF_SGPR_LD_NT  // A/B: streaming log-det stores
-      __builtin_nontemporal_store(ld[p], reinterpret_cast<f2*>(dst) + p);
-#else
       reinterpret_cast<float2*>(dst)[p] = float2{ld[p].x, ld[p].y};
-#endif
     }
   } else {
 #pragma unroll
@@ -358,12 +351,7 @@ __device__ __forceinline__ uint32_t load_labels(const int64_t* __restrict__ y, i
   for (int p = 0; p < P; ++p) {
     int lo0 = 0, hi0 = 0, lo1 = 0, hi1 = 0;
     if (rows == 2 * P && al16) {
-#ifdef CNF_SGPR_LAB_NT  // A/B: streaming label loads
-      using v4i = __attribute__((ext_vector_type(4))) int;
-      const v4i q = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(y32) + p);
-#else
       const int4 q = reinterpret_cast<const int4*>(y32)[p];
-#endif
       lo0 = q.x, hi0 = q.y, lo1 = q.z, hi1 = q.w;
     } else {
       if (2 * p < rows) lo0 = y32[4 * p], hi0 = y32[4 * p + 1];

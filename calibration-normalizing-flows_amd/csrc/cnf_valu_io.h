@@ -13,9 +13,6 @@
 #ifndef CNF_VALU_NT_STORE
 #define CNF_VALU_NT_STORE 1  // A/B: 0 = default-policy 16-B tile stores
 #endif
-#ifndef CNF_DPP_SUM
-#define CNF_DPP_SUM 1  // block_sum3's wave sums by DPP (0: __shfl_xor butterfly)
-#endif
 #ifndef CNF_VALU_NT_LOAD
 #define CNF_VALU_NT_LOAD 0  // A/B: streaming 16-B tile loads (every-layer pass 59.6 -> 65.1 us)
 #endif
@@ -250,22 +247,11 @@ __device__ __forceinline__ float wave_sum_dpp63(float v) {
 
 template <int ROWS>
 __device__ __forceinline__ void block_sum3(float a, float b, float c, float* sm, float* part) {
-#if CNF_DPP_SUM
   a = wave_sum_dpp63(a);
   b = wave_sum_dpp63(b);
   c = wave_sum_dpp63(c);
   const int tid = threadIdx.x, w = tid >> 6;
   constexpr int kLead = 63;  // the lane holding the wave's sums
-#else
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    a += __shfl_xor(a, off);
-    b += __shfl_xor(b, off);
-    c += __shfl_xor(c, off);
-  }
-  const int tid = threadIdx.x, w = tid >> 6;
-  constexpr int kLead = 0;
-#endif
   lds_barrier();
   if ((tid & 63) == kLead) {
     sm[4 * w] = a;
@@ -287,26 +273,16 @@ __device__ __forceinline__ void block_sum3(float a, float b, float c, float* sm,
 
 // The loss-term sums of nblk 16-B partial records by one 256-thread block
 // (threadIdx.x = t), in ONE fixed order: lane-strided sums with up to eight
-// records per lane in flight, an xor butterfly per wave, waves in index order.
-// k_reduce_rows4 (the follow-up launch) and k_sgpr's last block (the fused
-// hand-off) both sum this way, so either path gives the same bits.
+// records per lane in flight, a DPP sum per wave, waves in index order
+// (k_reduce_rows4, the follow-up launch of the fused eval passes).
+// An in-launch sum measured slower both ways it was tried (round 5-6,
+// DESIGN.md section 3): the last block found by a counter that every block
+// adds to (~1,500 returning atomics on one word at the end of a 2^20-row
+// call, +4.4 us), and a reducer block polling every block's tagged record
+// (no atomics, +0.3 us: the hand-off's latency equals the launch boundary).
 constexpr int kRR = 256;
-// record loads: plain (the follow-up launch), or device-coherent sc1 loads
-// (the in-kernel hand-off: they bypass the CU's L1, which may hold stale lines)
-struct LoadPlain {
-  __device__ float4 operator()(const float4* __restrict__ p, int b) const { return p[b]; }
-};
-struct LoadSc1 {
-  __device__ float4 operator()(const float4* __restrict__ p, int b) const {
-    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float4*>(p), 0, 0x7fffffff,
-                                                      0x00020000);
-    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, b * 16, 0, 16));
-  }
-};
-template <class LD = LoadPlain>
 __device__ __forceinline__ void reduce_rows4_block(const float4* __restrict__ partials, int nblk,
-                                                   float* __restrict__ out, float (*red)[3],
-                                                   LD ld = LD{}) {
+                                                   float* __restrict__ out, float (*red)[3]) {
   const int t = threadIdx.x;
   float s0 = 0.f, s1 = 0.f, s2 = 0.f;
   for (int b0 = t; b0 < nblk; b0 += 8 * kRR) {
@@ -314,7 +290,7 @@ __device__ __forceinline__ void reduce_rows4_block(const float4* __restrict__ pa
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int b = b0 + k * kRR;
-      v[k] = b < nblk ? ld(partials, b) : float4{0.f, 0.f, 0.f, 0.f};
+      v[k] = b < nblk ? partials[b] : float4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -323,20 +299,10 @@ __device__ __forceinline__ void reduce_rows4_block(const float4* __restrict__ pa
       s2 += v[k].z;
     }
   }
-#if CNF_DPP_SUM
   s0 = wave_sum_dpp63(s0);
   s1 = wave_sum_dpp63(s1);
   s2 = wave_sum_dpp63(s2);
   constexpr int kLead = 63;
-#else
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    s0 += __shfl_xor(s0, off);
-    s1 += __shfl_xor(s1, off);
-    s2 += __shfl_xor(s2, off);
-  }
-  constexpr int kLead = 0;
-#endif
   if ((t & 63) == kLead) {
     red[t >> 6][0] = s0;
     red[t >> 6][1] = s1;
@@ -348,59 +314,6 @@ __device__ __forceinline__ void reduce_rows4_block(const float4* __restrict__ pa
 #pragma unroll
     for (int w = 0; w < kRR / 64; ++w) a += red[w][t];
     out[t] = a;
-  }
-}
-
-// block_sum3 with the block-order sum done IN the launch by its last block
-// (no follow-up launch).  The hand-off is the sc1 form of
-// MI355X_MICROARCH.md's table (no release / acquire fences, which write back
-// and invalidate a whole L2): each block's thread 0 stores its record with an
-// sc1 (device-coherent) store, waits for it (vmcnt(0)), then adds 1 to the
-// arrival counter with a returning agent-scope atomic; the block whose add
-// returns nblk - 1 is last, and after a block barrier its threads read every
-// record with sc1 loads and sum them exactly as k_reduce_rows4 does (same
-// bits), then reset the counter.  Contract: *ctr is 0 before the launch (the
-// workspace's first word, zeroed once at allocation) and 0 after it.
-template <int ROWS>
-__device__ __forceinline__ void block_sum3_handoff(float a, float b, float c, float* sm,
-                                                   float* part, uint32_t* ctr, int nblk,
-                                                   float* __restrict__ out) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    a += __shfl_xor(a, off);
-    b += __shfl_xor(b, off);
-    c += __shfl_xor(c, off);
-  }
-  const int tid = threadIdx.x, w = tid >> 6;
-  lds_barrier();
-  if ((tid & 63) == 0) {
-    sm[4 * w] = a;
-    sm[4 * w + 1] = b;
-    sm[4 * w + 2] = c;
-  }
-  lds_barrier();
-  __shared__ int last;
-  if (tid == 0) {
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
-    for (int i = 0; i < ROWS / 64; ++i) {
-      s0 += sm[4 * i];
-      s1 += sm[4 * i + 1];
-      s2 += sm[4 * i + 2];
-    }
-    const auto rs = __builtin_amdgcn_make_buffer_rsrc(part, 0, 0x7fffffff, 0x00020000);
-    __builtin_amdgcn_raw_buffer_store_b128(
-        __builtin_bit_cast(__attribute__((ext_vector_type(4))) int, float4{s0, s1, s2, 0.f}), rs,
-        (int)blockIdx.x * 16, 0, 16);  // aux 16: sc1
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const uint32_t old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = old == (uint32_t)(nblk - 1);
-  }
-  __syncthreads();
-  if (last) {
-    static_assert(ROWS == kRR, "the hand-off reduces with the k_reduce_rows4 block shape");
-    reduce_rows4_block(reinterpret_cast<const float4*>(part), nblk, out,
-                       reinterpret_cast<float(*)[3]>(sm), LoadSc1{});
-    if (tid == 0) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 

@@ -24,6 +24,12 @@
 //     reference's at D=100.
 // f32 in / f32 accumulate is an exact fmaf chain (cdna_hip_programming.md,
 // FP32-input MFMA): the precision of the reference's fp32 addmm.
+//
+// The shipped library serves these shapes with k_wide16 (cnf_wide16.hip,
+// 16x16x4 tiles: 1.17x the reference's MACs instead of 1.39x, 0.72 of the
+// MFMA roof); this 32x32x2 family is compiled only into A/B builds
+// (make ab ABSRC=cnf_wide DEFS=-DCNF_WIDE16=0).  The shape table and the
+// wide_* dispatchers below are shared.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -32,8 +38,32 @@
 
 #include "cnf_internal.h"
 
+// CNF_WIDE16 (default 1): the wide_* entry points run k_wide16 (16x16x4
+// tiles, cnf_wide16.hip) for every shape of the table; 0 compiles and runs
+// k_wide's 32x32x2 tiles instead (A/B builds only).
+#ifndef CNF_WIDE16
+#define CNF_WIDE16 1
+#endif
+
 namespace cnf {
 namespace {
+
+// the shapes the register-MFMA family serves: CIFAR-100 flows (cfg4, and its
+// one- / no-hidden-layer variants) and the mid-width fixture shape
+struct WShape {
+  int D, H1, H2;
+};
+constexpr WShape kWShapes[] = {{100, 100, 100}, {100, 100, 0}, {100, 0, 0}, {32, 64, 64}};
+
+bool wshape(const Shape& s) {
+  if (s.n_lin > 3) return false;
+  const int h1 = s.n_lin >= 2 ? s.units[1] : 0, h2 = s.n_lin >= 3 ? s.units[2] : 0;
+  for (const WShape& e : kWShapes)
+    if (e.D == s.D && e.H1 == h1 && e.H2 == h2) return true;
+  return false;
+}
+
+#if !CNF_WIDE16
 
 typedef float v16 __attribute__((ext_vector_type(16)));
 
@@ -469,8 +499,7 @@ struct WEntry {
    {0, CNF_WG(D, H1, H2)::lin_off(1), CNF_WG(D, H1, H2)::lin_off(2)},             \
    CNF_WG(D, H1, H2)::mfmas(), fill_segment<D, H1, H2>}
 
-// CIFAR-100 flows (cfg4, and its one- / no-hidden-layer variants) and the
-// mid-width fixture shape
+// the kernels of every shape of kWShapes
 const WEntry kWTable[] = {
     CNF_WIDE(100, 100, 100),
     CNF_WIDE(100, 100, 0),
@@ -488,32 +517,32 @@ const WEntry* wfind(const Shape& s) {
 
 size_t wide_lds(const Shape& s) { return (size_t)kWWaves * (kWRows * (s.D | 1) + s.D) * 4; }
 
+#endif  // !CNF_WIDE16
+
 }  // namespace
 
-// CNF_WIDE16 (default): the wide_* entry points run k_wide16 (16x16x4 tiles,
-// cnf_wide16.hip) for every shape of the table; 0 keeps k_wide's 32x32x2
-// tiles (A/B builds).
-#ifndef CNF_WIDE16
-#define CNF_WIDE16 1
-#endif
-
 int64_t wide_layer_floats(const Shape& s) {
-  if (CNF_WIDE16) return wfind(s) ? wide16_layer_floats(s) : 0;
+#if CNF_WIDE16
+  return wshape(s) ? wide16_layer_floats(s) : 0;
+#else
   const WEntry* e = wfind(s);
   return e ? (int64_t)e->net_floats * s.nets : 0;
+#endif
 }
 
 // Final-output forward / inverse of shift-on, non-strict stacks in the table;
 // every-layer outputs and strict_nan stay on k_tile.
 bool wide_ok(const Shape& s) {
-  return wfind(s) && s.shift && !s.strict && !s.alt_mask && !s.s_tanh &&
+  return wshape(s) && s.shift && !s.strict && !s.alt_mask && !s.s_tanh &&
          !(s.options & CNF_OPT_NO_WIDE);
 }
 
 bool wide16_train_ok(const Shape& s) { return CNF_WIDE16 && wide_ok(s); }
 
 int wide_prepare(const Shape& s, const float* const* params, void* prepared, hipStream_t st) {
-  if (CNF_WIDE16) return wfind(s) ? wide16_prepare(s, params, prepared, st) : CNF_OK;
+#if CNF_WIDE16
+  return wshape(s) ? wide16_prepare(s, params, prepared, st) : CNF_OK;
+#else
   const WEntry* e = wfind(s);
   if (!e) return CNF_OK;
   float* region = reinterpret_cast<float*>(static_cast<char*>(prepared) + idx_bytes(s)) +
@@ -545,12 +574,15 @@ int wide_prepare(const Shape& s, const float* const* params, void* prepared, hip
     }
   }
   return CNF_OK;
+#endif
 }
 
 int wide_run(const Shape& s, const void* prepared, const float* in, float* out, float* ld,
              int64_t B, bool inverse, hipStream_t st, const float* log_priors) {
-  if (CNF_WIDE16) return wfind(s) ? wide16_run(s, prepared, in, out, ld, B, inverse, st, log_priors)
-                                  : CNF_ERR_UNSUPPORTED;
+#if CNF_WIDE16
+  return wshape(s) ? wide16_run(s, prepared, in, out, ld, B, inverse, st, log_priors)
+                   : CNF_ERR_UNSUPPORTED;
+#else
   const WEntry* e = wfind(s);
   if (!e) return CNF_ERR_UNSUPPORTED;
   const char* base = static_cast<const char*>(prepared);
@@ -569,6 +601,7 @@ int wide_run(const Shape& s, const void* prepared, const float* in, float* out, 
     return CNF_ERR_HIP;
   }
   return CNF_OK;
+#endif
 }
 
 }  // namespace cnf

@@ -158,11 +158,6 @@ __device__ __forceinline__ int feat_of(int s) {
   return u < G::DT ? u : -1;
 }
 
-// knock-out A/B builds only (results wrong): 1 no A-ring refills, 2 no
-// per-layer relayout in k_wide16, 4 no exp in the affine epilogue
-#ifndef CNF_W16_KO
-#define CNF_W16_KO 0
-#endif
 
 // A-operand ring depth: the deepest divisor of the layer's step count in
 // [6, pmax] (the ring runs on across layers)
@@ -179,8 +174,7 @@ template <class G, int NETS, int P, int T>
 __device__ __forceinline__ void refill(float (&ring)[P], const float* __restrict__ a,
                                        const float* __restrict__ an) {
   constexpr int LS = G::template lsp<NETS>();  // stream steps per layer (pads included)
-  if constexpr (CNF_W16_KO & 1) {
-  } else if constexpr (G::kLdsA) {
+  if constexpr (G::kLdsA) {
     static_assert(kPack4 && P % 4 == 0 && P <= kAC && LS % (2 * kAC) == 0, "LDS A stream");
     if constexpr ((T & 3) == 3) {
       constexpr int S0 = T - 3 + P;  // first step refilled
@@ -304,7 +298,7 @@ struct EpAffine {
       for (int q = 0; q < 4; ++q) {
         // padding slots get s = t = 0 (zero weights and bias): x stays x
         const float sv = s[g][q];
-        const float e = (CNF_W16_KO & 4) ? sv : __builtin_amdgcn_exp2f((INV ? -sv : sv) * 1.4426950408889634f);
+        const float e = __builtin_amdgcn_exp2f((INV ? -sv : sv) * 1.4426950408889634f);
         const float x = X[CT + MO][g][q];
         X[CT + MO][g][q] = INV ? (x - T[MO][g][q]) * e : fmaf(x, e, T[MO][g][q]);
         ld[g] += INV ? -sv : sv;
@@ -537,7 +531,7 @@ __global__ __launch_bounds__(64 * kWaves, kRunRG == 2 ? 2 : 1) void k_wide16(
     const int l = INV ? L - 1 - stp : stp;
     const int ln = stp + 1 < L ? (INV ? l - 1 : l + 1) : l;  // last layer: harmless re-read
     const int32_t* __restrict__ q = qtab + l * D;
-    if constexpr (INV && !(CNF_W16_KO & 2)) relayout<G>(st, qs, S, q, X, lane);  // flip / rev_perm first
+    if constexpr (INV) relayout<G>(st, qs, S, q, X, lane);  // flip / rev_perm first
     const float* __restrict__ wl = W + (int64_t)l * LF + kLaneStride * lane;
     const float* __restrict__ wn = W + (int64_t)ln * LF + kLaneStride * lane;
     const float* __restrict__ bl = W + (int64_t)l * LF + LA;  // the layer's bias blocks
@@ -555,7 +549,7 @@ __global__ __launch_bounds__(64 * kWaves, kRunRG == 2 ? 2 : 1) void k_wide16(
         for (int g = 0; g < kRunRG; ++g) X[CT + t][g] = INV ? X[CT + t][g] - Tv[t][g] : X[CT + t][g] + Tv[t][g];
     }
     pad_steps<G, NETS, P>(ring, wl, wn, std::make_integer_sequence<int, LSP - NETS * G::steps()>{});
-    if constexpr (!INV && !(CNF_W16_KO & 2)) relayout<G>(st, qs, S, q, X, lane);  // perm then flip
+    if constexpr (!INV) relayout<G>(st, qs, S, q, X, lane);  // perm then flip
   }
   if constexpr (G::kLdsA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the block
 

@@ -335,6 +335,13 @@ struct DwArgs {
   int64_t M, rows, PS;
 };
 
+// CNF_WDW16 (default 1): the layer-at-a-time weight gradients on k_wdw16's
+// 16x16x4 tiles; 0 compiles and runs k_wdw's 32x32x2 predecessor instead
+// (A/B builds only: make ab ABSRC=cnf_wvjp DEFS=-DCNF_WDW16=0)
+#ifndef CNF_WDW16
+#define CNF_WDW16 1
+#endif
+#if !CNF_WDW16
 constexpr int kDwCT = 4;  // column tiles per wave (128 columns)
 
 __global__ __launch_bounds__(256, 3) void k_wdw(DwArgs da) {
@@ -441,6 +448,8 @@ __global__ __launch_bounds__(256, 3) void k_wdw(DwArgs da) {
     }
   }
 }
+
+#endif  // !CNF_WDW16
 
 // The same weight gradients on v_mfma_f32_16x16x4f32 tiles (the same 64
 // FLOP/clk/SIMD as 32x32x2): a wave still owns 32 output rows, and up to 112
@@ -677,9 +686,6 @@ __device__ __forceinline__ void wdwg_chunks(const DwJob& j, float* sm, int w, in
 #endif
 // A/B timing only (wrong results): 1 = no MFMAs, 2 = no operand DMA (the
 // MFMAs run on whatever the LDS stages hold)
-#ifndef CNF_WDWG_KO
-#define CNF_WDWG_KO 0
-#endif
 template <int NTG, int NTH, int W>
 __device__ __forceinline__ void wdwg_rr(const DwJob& j, const DwArgs& da, float* sm, int lane,
                                         int64_t r0, int nch) {
@@ -691,7 +697,6 @@ __device__ __forceinline__ void wdwg_rr(const DwJob& j, const DwArgs& da, float*
 #pragma unroll
   for (int m = 0; m < NP; ++m) acc[m] = f4{};
   auto dma = [&](int c, int stg) {
-    if (CNF_WDWG_KO == 2) return;
     const float* gsrc = j.G + ((r0 >> 5) + c) * 32 * ldg;
     const float* hsrc = j.H + ((r0 >> 5) + c) * 32 * ldh;
     float* dst = sm + stg * TPC * 512;
@@ -720,10 +725,7 @@ __device__ __forceinline__ void wdwg_rr(const DwJob& j, const DwArgs& da, float*
 #pragma unroll
       for (int m = 0; m < NP; ++m) {
         const int p = W + 4 * m;
-        if (CNF_WDWG_KO == 1)
-          acc[m][0] += a[p / NTH] * b[p % NTH];
-        else
-          acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[p / NTH], b[p % NTH], acc[m], 0, 0, 0);
+        acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[p / NTH], b[p % NTH], acc[m], 0, 0, 0);
       }
     }
   }
@@ -809,9 +811,6 @@ __global__ __launch_bounds__(256, 2) void k_wdw16g(DwArgs da) {
   }
 }
 
-#ifndef CNF_WDW16
-#define CNF_WDW16 1  // A/B: 0 keeps the 32x32 tiles of k_wdw
-#endif
 #ifndef CNF_WDW16G
 #define CNF_WDW16G 1  // A/B: 0 runs the fused sweeps' weight gradients on k_wdw16
 #endif
@@ -1716,12 +1715,19 @@ struct Runner {
         j.gcl = j.N - 1;
         j.hcl = (int)j.ldh - 1;
         j.slot = 0;
-        const int ncg = CNF_WDW16 ? ((j.K + 1 + 15) / 16 + kDw16CT - 1) / kDw16CT
-                                  : (j.tiles_c + kDwCT - 1) / kDwCT;
+#if CNF_WDW16
+        const int ncg = ((j.K + 1 + 15) / 16 + kDw16CT - 1) / kDw16CT;
+#else
+        const int ncg = (j.tiles_c + kDwCT - 1) / kDwCT;
+#endif
         max_subs = std::max(max_subs, ((j.N + 127) / 128) * ncg);
       }
     }
-    hipLaunchKernelGGL(CNF_WDW16 ? k_wdw16 : k_wdw,
+#if CNF_WDW16
+    hipLaunchKernelGGL(k_wdw16,
+#else
+    hipLaunchKernelGGL(k_wdw,
+#endif
                        dim3((unsigned)p.nkb, (unsigned)jobs, (unsigned)max_subs), dim3(256), 0, st,
                        da);
     reduce_partials(part, (int)p.nkb, (int)PS, (int)PL, grads_layer, nullptr, st);

@@ -216,6 +216,18 @@ int cnf_adam_step_sched(const cnf_desc* desc, float* const* params, const float*
                         float* exp_avg, float* exp_avg_sq, const float* sched, double beta1,
                         double beta2, double eps, double weight_decay, void* stream);
 
+/* cnf_adam_step (sched == NULL: step and lr as there) or cnf_adam_step_sched
+ * (sched != NULL: step and lr ignored) that first reads the DEVICE int32
+ * *skip_flag -- the flag cnf_guard_nonfinite ORs into -- and, when it is
+ * non-zero, updates nothing: the parameters and both moments keep the last
+ * finite step's values, as the reference keeps its weights when it breaks out
+ * of the loop before opt.step() on NaN (run_experiment3D.py:129-133).  No host
+ * sync: the guard's scan of the gradient and this step queue on one stream. */
+int cnf_adam_step_guarded(const cnf_desc* desc, float* const* params, const float* grads,
+                          float* exp_avg, float* exp_avg_sq, int64_t step, double lr,
+                          const float* sched, double beta1, double beta2, double eps,
+                          double weight_decay, const int32_t* skip_flag, void* stream);
+
 /* Device-side non-finite guard (failure detection; the counterpart of the
  * reference's NaN abort, run_experiment3D.py:129-131, without a host sync):
  * scans n floats of a DEVICE array (z, logdet, loss_terms, gradients ...) and

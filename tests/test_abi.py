@@ -177,3 +177,35 @@ def test_guard_argument_validation_without_gpu():
     assert lib.cnf_guard_nonfinite(P(ctypes.addressof(buf) + 2), ctypes.c_int64(4),
                                    P(ctypes.addressof(flag)), P(0)) == -6
     assert lib.cnf_guard_nonfinite(P(0), ctypes.c_int64(0), P(ctypes.addressof(flag)), P(0)) == 0
+
+
+def test_adam_guarded_argument_validation_without_gpu():
+    """cnf_adam_step_guarded needs its skip flag (NULL is rejected before any
+    launch; the plain cnf_adam_step is the unguarded form)."""
+    lib = _lib.lib()
+    stack = CouplingStack([NvpCouplingLayer(10, [5, 5]) for _ in range(2)])
+    P = ctypes.c_void_p
+    arr = (P * 24)()  # 2 layers x 2 nets x 3 Linears x (W, b); never read
+    st = lib.cnf_adam_step_guarded(ctypes.byref(stack.desc), arr, P(16), P(16), P(16),
+                                   ctypes.c_int64(1), ctypes.c_double(1e-3), None,
+                                   ctypes.c_double(0.9), ctypes.c_double(0.999),
+                                   ctypes.c_double(1e-8), ctypes.c_double(0.0), None, P(0))
+    assert st == -1
+
+
+def test_roctx_build_exports_every_header_symbol():
+    """`make roctx` (the traced diagnostic build): the same C ABI, with every
+    launching entry point inside a roctx range, linked against the roctx
+    library (checked by symbol tables only: no GPU, no tracer needed)."""
+    import subprocess
+    path = os.path.join(ROOT, "calibration-normalizing-flows_amd", "cnf_hip",
+                        "libcnf_hip_roctx.so")
+    if not os.path.exists(path):
+        pytest.skip("make roctx was not run")
+    syms = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True,
+                          check=True).stdout
+    for name in header_functions():
+        assert re.search(r"\sT %s$" % name, syms, re.M), name
+    undef = subprocess.run(["nm", "-D", "--undefined-only", path], capture_output=True,
+                           text=True, check=True).stdout
+    assert "roctxRangePushA" in undef and "roctxRangePop" in undef

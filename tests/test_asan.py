@@ -29,7 +29,7 @@ def _runtime():
 def asan_build():
     if _runtime() is None:
         pytest.skip("clang ASan runtime not found")
-    r = subprocess.run(["make", "-C", CSRC, "asan"], capture_output=True, text=True, timeout=1800)
+    r = subprocess.run(["make", "-C", CSRC, "-j8", "asan"], capture_output=True, text=True, timeout=1800)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     return True
 

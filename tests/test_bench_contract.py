@@ -123,3 +123,46 @@ def test_nll_all_reduce_buckets_cover_every_batch_once(monkeypatch):
                 for k, (what, vals) in enumerate(log):
                     if what == "reduce" and vals and vals[0] + 2 * bench.NLL_BUCKET < steps:
                         assert ("wait", vals) in log[k + 1:], (steps, vals)
+
+
+def test_nll_all_reduce_realigns_after_uncollected_batches(monkeypatch):
+    """The bench's own order: settle() and kernel_only_seconds()
+    launch batches WITHOUT the collective, then timed() runs warmup + drain and
+    the timed steps + drain.  Every batch launched under the collective must be
+    reduced exactly once, and no batch launched without it may be reduced."""
+    import torch
+
+    class FakeRunner:
+        def __init__(self):
+            self.term_bufs = torch.zeros(2, bench.NLL_BUCKET, 3)
+            self.i = 0
+
+        def step(self):
+            self.terms = self.term_bufs[(self.i // bench.NLL_BUCKET) % 2,
+                                        self.i % bench.NLL_BUCKET]
+            self.terms.fill_(float(self.i))
+            self.i += 1
+
+    reduced = []
+
+    def fake_all_reduce(t, async_op=False):
+        reduced.extend(int(v) for v in t[:, 0].tolist())
+
+    monkeypatch.setattr(bench.dist, "all_reduce", fake_all_reduce)
+    for pre in (0, 3, 17, bench.NLL_BUCKET + 9):
+        for warm, steps in ((2, 7), (5, bench.NLL_BUCKET + 4), (0, 2 * bench.NLL_BUCKET)):
+            reduced.clear()
+            r = FakeRunner()
+            coll = bench.NllAllReduce(r)
+            for _ in range(pre):  # settle: no collective
+                r.step()
+            expect = []
+            coll.realign()  # as timed(): once, then warmup + drain, steps + drain
+            for n in (warm, steps):
+                first = r.i
+                for _ in range(n):
+                    r.step()
+                    coll()
+                expect.extend(range(first, r.i))
+                coll.drain()
+            assert sorted(reduced) == expect, (pre, warm, steps)

@@ -21,6 +21,9 @@
 #   abwide       tools/ab/ab_wide_train.py (cfg4 training step) for the shipped lib and every tools/ab/lib*.so, x3
 #   abvjp        tools/ab/ab_vjp.py (cfg2 training step + gradient checksum) for the shipped lib and every tools/ab/lib*.so, x3
 #   abterms      tools/ab/ab_terms.py (loss-term bits + fp64 check) for every tools/ab/lib*.so
+#   roctx        rocprofv3 marker + kernel trace of the roctx-ranged build (make roctx)
+#   prof:<wl>:<mode>:<n>  kernel trace of tools/prof_target.py (clock settled first) and
+#                tools/trace_stats.py over its last n calls
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -102,7 +105,11 @@ for step in "$@"; do
     prof:*)  # prof:<workload>:<mode>:<launches> -> gpurun_out/prof_<workload>_<mode>/
       IFS=: read -r _ wl md nl <<< "$step"
       rm -rf gpurun_out/prof_${wl}_${md}
-      run prof_${wl}_${md} 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${wl}_${md} -o run --output-format csv -- python tools/prof_target.py --workload $wl --mode $md --launches $nl ;;
+      run prof_${wl}_${md} 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${wl}_${md} -o run --output-format csv -- python tools/prof_target.py --workload $wl --mode $md --launches $nl &&
+      python tools/trace_stats.py gpurun_out/prof_${wl}_${md}/run_kernel_trace.csv $nl gpurun_out/prof_${wl}_${md}/settled_stats.csv ;;
+    roctx)  # the traced build's ranges beside its kernels (make roctx)
+      rm -rf gpurun_out/roctx
+      CNF_HIP_LIB=$PWD/calibration-normalizing-flows_amd/cnf_hip/libcnf_hip_roctx.so run roctx 300 rocprofv3 --marker-trace --kernel-trace --stats -d gpurun_out/roctx -o run --output-format csv -- python tools/prof_target.py --mode loss --launches 20 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

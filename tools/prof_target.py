@@ -18,6 +18,9 @@ ap.add_argument("--workload", default="cfg2")
 ap.add_argument("--launches", type=int, default=40)
 ap.add_argument("--batch", type=int, default=0)
 ap.add_argument("--mode", default="loss", choices=["loss", "forward", "all", "train", "calib"])
+ap.add_argument("--settle-s", type=float, default=0.3,
+                help="untimed launches for this long first, as bench.py settles the clock; "
+                     "tools/trace_stats.py keeps only the last --launches calls")
 a = ap.parse_args()
 w = dict(bench.WORKLOADS[a.workload])
 if a.batch:
@@ -38,6 +41,12 @@ elif a.mode == "train":
     flow = bench.make_flow(w, dev)
     stack = flow._native_stack()
     x, y = bench.synthetic_logits(w["B"], w["D"], dev, 4321)
+    import time
+    t0 = time.perf_counter()
+    while a.settle_s > 0 and time.perf_counter() - t0 < a.settle_s:
+        for _ in range(8):
+            V.loss_and_grads(stack, x, y, grad_scale=1.0 / w["B"])
+        torch.cuda.synchronize()
     for _ in range(a.launches):
         V.loss_and_grads(stack, x, y, grad_scale=1.0 / w["B"])
     name = stack.kernel_name()
@@ -47,6 +56,8 @@ else:
         mode = "forward"
     r = bench.Runner(w, dev, 1.5e9, all_outputs=(mode == "all"),
                      mode="loss" if mode == "loss" else "forward")
+    if a.settle_s > 0:
+        r.settle(a.settle_s)
     for _ in range(a.launches):
         r.step()
     name = r.stack.kernel_name()
