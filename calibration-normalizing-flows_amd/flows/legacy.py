@@ -53,11 +53,16 @@ zero-embedding them into the maintained NICE layer (_EmbeddedNice):
 * version 1 (even D): with R the full reversal, a split layer in 'odd' mode
   is M_g(R x) and in 'even' mode R M_f(x), where M is the maintained layer and
   g is f with its input columns and output rows reversed; the stack is
-  R^[L even] M_{f_{L-1}} ... M_{f_1} M_{g_0} (R x).
-Odd-D version 1 (its 'odd' layers transform the larger half) keeps the torch
-restatement, reported through flows.flows._not_native.  Version 3 is the
-alternate-mask stack of the RealNVP path with the s-net absent, so it runs
-natively as CNF_OPT_ALT_MASK on the shift-only kernels.
+  R^[L even] M_{f_{L-1}} ... M_{f_1} M_{g_0} (R x);
+* version 1, odd D = 2h+1 (code-old/nice.py:140-155: its 'odd' layers add
+  f(x1) to the LARGER half x2, h+1 features, which no mask of width D can
+  express): the same stack over D+1 features, x' = [x1, 0, x2] -- a zero
+  feature d appended to x1.  Both halves then hold h+1 features; in an 'odd'
+  layer d is an input of f (a zero weight column), in an 'even' layer an
+  output (a zero weight row and bias, so d stays exactly 0); the output drops
+  d again.
+Version 3 is the alternate-mask stack of the RealNVP path with the s-net
+absent, so it runs natively as CNF_OPT_ALT_MASK on the shift-only kernels.
 """
 import torch
 import torch.nn.functional as F
@@ -319,11 +324,15 @@ class _EmbeddedNice:
     refreshed from the half-width Keras conditioners whenever one of their
     parameters changed (in-place version counters); hidden Linears are the
     conditioners' own tensors.  rev[l]: layer l's conditioner enters with its
-    input columns and output rows reversed (version 1, even layers)."""
+    input columns and output rows reversed (version 1, even layers).  pad:
+    version 1 with odd D runs over D + 1 features (the zero feature d after
+    x1; module docstring)."""
 
     def __init__(self, flow, device):
         self.flow = flow
-        D, h = flow.dim, flow.dim // 2
+        self.pad = 1 if (flow.version == 1 and flow.dim % 2) else 0
+        D = flow.dim + self.pad  # the virtual stack's width
+        h = D // 2
         self.D, self.h = D, h
         self.rev = [flow.version == 1 and l % 2 == 0 for l in range(len(flow.layers))]
         vls, self.fparams, self.bufs = [], [], []
@@ -350,36 +359,41 @@ class _EmbeddedNice:
     def key(self):
         return tuple((p.data_ptr(), p._version) for p in self.fparams)
 
+    def _cols(self, rev):
+        """First column of the conditioning block that holds f's inputs: with
+        the pad, a reversed ('odd' mode) layer sees [d, x1 reversed] there."""
+        return self.h + (self.pad if rev else 0)
+
     @torch.no_grad()
     def refresh(self):
         k = self.key()
         if k == self._key:
             return
-        h = self.h
         for ly, (W0, WL, bL), rev in zip(self.flow.layers, self.bufs, self.rev):
             lins = list(ly.f)
             first, last = lins[0], lins[-1]
+            c0, n_out = self._cols(rev), last.weight.shape[0]
             if len(lins) > 1:
-                W0[:, h:].copy_(first.weight.flip(1) if rev else first.weight)
-                WL[:h].copy_(last.weight.flip(0) if rev else last.weight)
-                bL[:h].copy_(last.bias.flip(0) if rev else last.bias)
+                W0[:, c0:].copy_(first.weight.flip(1) if rev else first.weight)
+                WL[:n_out].copy_(last.weight.flip(0) if rev else last.weight)
+                bL[:n_out].copy_(last.bias.flip(0) if rev else last.bias)
             else:
                 w = first.weight.flip(0).flip(1) if rev else first.weight
                 W0.zero_()
-                W0[:h, h:].copy_(w)
+                W0[:n_out, c0:].copy_(w)
                 bL.zero_()
-                bL[:h].copy_(first.bias.flip(0) if rev else first.bias)
+                bL[:n_out].copy_(first.bias.flip(0) if rev else first.bias)
         self._key = k
 
     def grads_back(self, flat):
         """Flat gradient of the virtual stack (ABI order) -> per-parameter
         gradients of the Keras conditioners (fparams order)."""
-        h = self.h
         out_w, out_b = [], []
         off = 0
         for ly, rev in zip(self.flow.layers, self.rev):
             lins = list(ly.f)
             gw, gb = [], []
+            c0, n_out = self._cols(rev), lins[-1].weight.shape[0]
             for i, lin in enumerate(lins):
                 n_out_full = self.D if (i == len(lins) - 1) else lin.weight.shape[0]
                 n_in_full = self.D if i == 0 else lin.weight.shape[1]
@@ -388,9 +402,9 @@ class _EmbeddedNice:
                 b = flat[off:off + n_out_full]
                 off += n_out_full
                 if i == 0:
-                    W = W[:, h:]
+                    W = W[:, c0:]
                 if i == len(lins) - 1:
-                    W, b = W[:h], b[:h]
+                    W, b = W[:n_out], b[:n_out]
                 if rev and i == 0:
                     W = W.flip(1)
                 if rev and i == len(lins) - 1:
@@ -469,10 +483,6 @@ class LegacyNiceFlow(nn.Module):
                 and x.dim() == 2 and x.shape[1] == self.dim):
             return False
         from flows.flows import _not_native
-        if self.version == 1 and self.dim % 2:
-            _not_native("legacy NiceFlow version 1 with odd D (its 'odd' layers transform "
-                        "the larger half)")
-            return False
         if self.layers[0].activation != "relu":
             _not_native("legacy NICE activation %r" % self.layers[0].activation)
             return False
@@ -499,6 +509,9 @@ class LegacyNiceFlow(nn.Module):
         post = (self.version == 1 and L % 2 == 0) or (self.version == 2 and L % 2 == 1)
         if inverse:
             pre, post = post, pre
+        h0 = self.dim // 2
+        if emb.pad:  # x' = [x1, d = 0, x2]
+            x = torch.cat([x[:, :h0], x.new_zeros(x.shape[0], 1), x[:, h0:]], dim=1)
         if pre:
             x = x.flip(1)
         fparams = emb.fparams
@@ -509,6 +522,8 @@ class LegacyNiceFlow(nn.Module):
             y, ld, _ = emb.stack.run(x.contiguous(), inverse=inverse)
         if post:
             y = y.flip(1)
+        if emb.pad:  # drop d (exactly 0 throughout)
+            y = torch.cat([y[:, :h0], y[:, h0 + 1:]], dim=1)
         return y, ld
 
     def invalidate_native(self):

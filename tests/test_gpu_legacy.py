@@ -132,6 +132,9 @@ def test_legacy_nice_v3_native_matches_restatement(D, L, hidden):
     (1, 10, 4, [10]),     # code-old/nice.py NiceFlow defaults: hidden [dim], layers 4
     (1, 6, 3, [5, 5]),    # odd L: one more reversal
     (1, 4, 2, []),        # one Linear per conditioner
+    (1, 7, 3, [5, 5]),    # odd D: 'odd' layers add to the larger half (padded stack)
+    (1, 3, 4, [3]),       # odd D, even L, hidden [dim]
+    (1, 5, 1, []),        # odd D, one Linear
     (2, 10, 4, [10]),     # NiceFlow_v2
     (2, 7, 3, [5, 5]),    # odd D, odd L
     (2, 3, 2, []),
@@ -189,10 +192,12 @@ def test_legacy_nice_split_versions_native(version, D, L, hidden):
     assert _rel(y2.cpu(), y2_ref) <= 1e-5
 
 
-def test_legacy_nice_v1_odd_dim_reports_torch_execution():
+def test_legacy_nice_v1_odd_dim_is_native():
     """NiceFlow (version 1) with odd D transforms the larger half in its 'odd'
-    layers, which the maintained layer cannot express: it runs torch ops on
-    the GPU and says so, with results equal to the CPU restatement."""
+    layers (code-old/nice.py:140-155); it runs natively over the D + 1-wide
+    padded stack (flows/legacy.py) with no torch-ops warning, and equals the
+    CPU restatement (parity unpinned: TensorFlow absent)."""
+    import warnings
     from flows.legacy import LegacyNiceFlow
     import flows.flows as FF
     torch.manual_seed(0)
@@ -202,7 +207,10 @@ def test_legacy_nice_v1_odd_dim_reports_torch_execution():
         y_ref, _ = f(x)
     fg = f.to(DEV)
     FF._warned.clear()
-    with pytest.warns(RuntimeWarning, match="version 1 with odd D"):
+    n0 = engine.stats["forward"]
+    with warnings.catch_warnings():
+        warnings.simplefilter("error", RuntimeWarning)
         with torch.no_grad():
             y, _ = fg(x.to(DEV))
+    assert engine.stats["forward"] > n0, "native path did not run"
     assert _rel(y.cpu(), y_ref) <= 1e-5

@@ -270,10 +270,39 @@ def test_strict_vjp_off_the_narrow_path(name, objective):
         _same(torch.zeros_like(r) if gg is None else gg, r, "grad %d" % i)
 
 
+def _syn_inv_case(name, B=96):
+    """_syn_case for the INVERSE: the inverse runs the last layer
+    first, so that layer's s-net is pushed instead -- its last output below
+    -89 in about half of the rows, where exp(-s) overflows and the masked
+    features read 0 * inf = NaN (flows/flows.py:123), the other rows finite."""
+    meta, state, x, _ = _syn_case(name, B)
+    z = x / 8.0
+    if meta["scale"]:
+        L = meta["L"]
+        pre = "layers.%d.s." % (L - 1)
+        wk = [k for k in state if k.startswith(pre) and k.endswith("weight")][-1]
+        bk = wk[:-len("weight")] + "bias"
+        ff = build_flow(meta, state, "cpu")
+        last = [m for m in ff.layers[L - 1].s.modules() if isinstance(m, torch.nn.Linear)][-1]
+        got = {}
+        def keep_input(m, i, o):
+            got.setdefault("h", i[0].detach())
+        hk = last.register_forward_hook(keep_input)
+        with torch.no_grad():
+            ff.layers[L - 1].backward(z)  # the inverse's first step (flows/flows.py:114-126)
+        hk.remove()
+        u = got["h"] @ torch.from_numpy(state[wk][-1]).float()
+        a = 40.0 / (float(u.std()) + 1e-6)
+        state[wk] = state[wk].copy()
+        state[bk] = state[bk].copy()
+        state[wk][-1] *= a
+        state[bk][-1] = -89.0 - a * float(u.median())
+    return meta, state, z
+
+
 @pytest.mark.parametrize("name", sorted(_SYN))
 def test_strict_inverse_vjp_off_the_narrow_path(name):
-    meta, state, x, _ = _syn_case(name)
-    z = x / 8.0
+    meta, state, z = _syn_inv_case(name)
     f_cpu = build_flow(meta, state, "cpu", strict_nan=True)
     zc = z.clone().requires_grad_(True)
     ref_out = _inv_xs_objective(f_cpu, zc)
@@ -287,6 +316,9 @@ def test_strict_inverse_vjp_off_the_narrow_path(name):
     ps = [p for p in f.parameters() if p.requires_grad]
     got = torch.autograd.grad(out, ps + [zz], allow_unused=True)
     torch.cuda.synchronize()
+    if meta["scale"]:  # the case must mix NaN / inf and finite rows
+        bad = ~torch.isfinite(ref[-1]).all(1)
+        assert bad.any() and not bad.all(), (name, int(bad.sum()))
     _same(out, ref_out.detach(), "objective")
     for k, (g, r) in enumerate(zip(got, ref)):
         _same(torch.zeros_like(r) if g is None else g, r, "grad %d" % k)

@@ -259,3 +259,49 @@ def test_fused_wide_training_matches_layerwise_path(flip):
     rel = (d1 - d2).abs().amax(1) / (d2.abs().amax(1) + 1e-30)
     assert int((rel > 1e-5).sum()) <= max(2, B // 4000), rel.topk(5)
     assert not torch.equal(g1, g2), "both runs took the same path"
+
+
+@pytest.mark.parametrize("act_scale", [1e-9, 1e-12])
+def test_fused_loss_grads_tiny_activations_small_grad_scale(act_scale):
+    """k_vjp2 accumulates the hidden columns' weight gradients against
+    h' = 2^-64 h and applies the 2^64 once per wave (cnf_vjp2.h): a product
+    g * h' falls into the fp32 denormal range when |g h| < 2^-62.  Held to the
+    reference's own fp32 autograd where that happens -- grad_scale 2^-23 (a
+    2^23-row batch) and hidden activations of ~1e-9 / 1e-12 (products ~1e-16 /
+    1e-19 per row) -- at the same 1e-4 bar as every other gradient."""
+    from flows.flows import Flow, NvpCouplingLayer
+    torch.manual_seed(11)
+    f = Flow([NvpCouplingLayer(10, [5, 5]) for _ in range(3)])
+    g = torch.Generator().manual_seed(12)
+    with torch.no_grad():
+        for k, p in f.named_parameters():
+            if not p.requires_grad:
+                continue
+            v = torch.randn(p.shape, generator=g) * 0.3
+            if k.endswith("layers.0.weight") or k.endswith("layers.0.bias"):
+                v = v.abs() * act_scale if k.endswith("bias") else v * act_scale
+            p.copy_(v)
+    B = 4096
+    x = torch.randn(B, 10, generator=torch.Generator().manual_seed(13))
+    y = torch.randint(0, 10, (B,), generator=torch.Generator().manual_seed(14))
+    gs = 2.0 ** -23
+    xc = x.clone()
+    zs, ld = f(xc)
+    p_y = torch.softmax(zs[-1], 1).gather(1, y[:, None]).squeeze(1)
+    loss = (-(torch.log(p_y + 1e-7) + ld)).sum() * gs   # calibrators.py:288-291, scaled
+    loss.backward()
+    ref = {k: p.grad.clone() for k, p in f.named_parameters() if p.requires_grad}
+    fg = f.to(DEV)
+    stack = fg._native_stack()
+    terms, grads, _ = V.loss_and_grads(stack, x.to(DEV), y.to(DEV), kind=0, det=1.0,
+                                       grad_scale=gs)
+    worst, where = 0.0, None
+    for (k, p), gg in zip([(k, p) for k, p in fg.named_parameters() if p.requires_grad],
+                          V._split(stack, grads)):
+        a, b = gg.cpu().numpy(), ref[k].numpy()
+        # relative to the tensor's own scale (no absolute floor: these
+        # gradients are ~1e-16 and smaller)
+        e = float(np.max(np.abs(a - b))) / max(float(np.max(np.abs(b))), 1e-37)
+        if e > worst:
+            worst, where = e, k
+    assert worst <= 1e-4, (worst, where)

@@ -228,3 +228,54 @@ def test_legacy_nice_split_equals_embedded_maintained_stack(version, D, L, hidde
         if (version == 1 and L % 2 == 0) or (version == 2 and L % 2 == 1):
             z = z.flip(1)
     assert (z - y_ref).abs().max().item() <= 1e-12
+
+
+@pytest.mark.parametrize("D,L,hidden", [(3, 1, []), (3, 2, [3]), (7, 3, [5, 5]), (5, 4, [4]),
+                                        (9, 5, [])])
+def test_legacy_nice_v1_odd_dim_equals_padded_embedded_stack(D, L, hidden):
+    """Odd-D NiceFlow (code-old/nice.py:140-155: the 'odd' layers add f(x1)
+    to the larger half x2) as the native path runs it, in float64 on the CPU:
+    the maintained additive stack over D + 1 features, x' = [x1, 0, x2], the
+    zero feature an input of every 'odd' layer's conditioner (zero column) and
+    an output of every 'even' layer's (zero row and bias); it stays exactly 0
+    and the output drops it."""
+    from flows.legacy import LegacyNiceFlow, _EmbeddedNice
+    torch.manual_seed(0)
+    f = LegacyNiceFlow(D, layers=L, hidden_size=hidden, version=1).double()
+    with torch.no_grad():
+        for p in f.parameters():
+            p.copy_(torch.randn_like(p) * 0.3)
+    x = torch.randn(7, D, dtype=torch.float64)
+    with torch.no_grad():
+        y_ref, _ = f(x)
+        emb = _EmbeddedNice(f, "cpu")
+        assert emb.pad == 1 and emb.D == D + 1
+        for bufs in emb.bufs:
+            for t in bufs:
+                if t is not None:
+                    t.data = t.data.double()
+        emb.refresh()
+        h0, Dp = D // 2, D + 1
+        z = torch.cat([x[:, :h0], torch.zeros(7, 1, dtype=torch.float64), x[:, h0:]], 1).flip(1)
+        h = Dp // 2
+        mask = torch.zeros(1, Dp, dtype=torch.float64)
+        mask[:, h:] = 1
+        for vl in emb.stack.layers:
+            a = mask * z
+            for i, lin in enumerate(vl.t.layers):
+                a = a @ lin.weight.t() + lin.bias
+                if i < len(vl.t.layers) - 1:
+                    a = torch.relu(a)
+            z = (mask * z + (1 - mask) * (z + a)).flip(1)
+        if L % 2 == 0:
+            z = z.flip(1)
+        assert z[:, h0].abs().max().item() == 0.0
+        y = torch.cat([z[:, :h0], z[:, h0 + 1:]], 1)
+    assert (y - y_ref).abs().max().item() <= 1e-12
+    # the gradient map: a flat gradient of the virtual stack equal to its own
+    # parameters maps back onto the conditioners' own tensors
+    flat = torch.cat([t.reshape(-1) for vl in emb.stack.layers for lin in vl.t.layers
+                      for t in (lin.weight, lin.bias)])
+    back = emb.grads_back(flat)
+    for got, p in zip(back, emb.fparams):
+        assert torch.equal(got, p.detach())
