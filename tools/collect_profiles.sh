@@ -7,9 +7,14 @@ TAG=$1
 cd "$(dirname "$0")/.."
 mkdir -p profiles
 cp gpurun_out/prof_${TAG}/run_kernel_stats.csv profiles/${TAG}_bench_kernel_stats.csv
+[ -f gpurun_out/prof_${TAG}/settled_stats.csv ] && cp gpurun_out/prof_${TAG}/settled_stats.csv profiles/${TAG}_bench_settled_stats.csv
 for d in gpurun_out/prof_${TAG}_*; do
   n=${d#gpurun_out/prof_${TAG}_}
   [ -f $d/run_kernel_stats.csv ] && cp $d/run_kernel_stats.csv profiles/${TAG}_${n}_kernel_stats.csv
+  [ -f $d/settled_stats.csv ] && cp $d/settled_stats.csv profiles/${TAG}_${n}_settled_stats.csv
+done
+for m in loss fwd; do
+  [ -f gpurun_out/sweep_$m.log ] && grep '^{' gpurun_out/sweep_$m.log > profiles/${TAG}_batch_sweep_$m.jsonl
 done
 for spec in "cfg2 loss k_sgpr 1048576" "cfg2 all k_valu 1048576" "cfg2 train k_vjp2 1048576" "cfg4 forward k_wide16 262144" "cfg4 train k_wdw16 262144" "cfg4 train k_wtrain16_fwd 262144" "cfg4 train k_wtrain16_bwd 262144"; do
   set -- $spec

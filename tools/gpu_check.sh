@@ -23,12 +23,19 @@ run smoke 400 python -c "import __graft_entry__ as g; g.smoke()"
 TAILN=12 CNF_RECORD_DIR=gpurun_out run pytest_gpu 900 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread
 TAILN=2 run bench 600 python bench.py
 [ -n "$QUICK" ] && exit 0
-run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python bench.py --steps 100 --no-cpu-baseline --no-variants
-# one kernel-trace summary per profiled pass
-for spec in "cfg2 loss" "cfg2 forward" "cfg2 all" "cfg5 forward" "cfg4 forward" "cfg2 train" "cfg4 train"; do
+run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python bench.py --steps 200 --no-cpu-baseline --no-variants
+# the bench's own timed steps: its last 200 + 100 calls (the timed region and
+# the kernel-only pass, both after the settle and the warmup)
+python tools/trace_stats.py gpurun_out/prof_$TAG/run_kernel_trace.csv 300 gpurun_out/prof_$TAG/settled_stats.csv
+# one kernel-trace summary per profiled pass, the clock settled first (0.3 s,
+# as bench.py), statistics over the last N calls only (tools/trace_stats.py)
+for spec in "cfg2 loss 200" "cfg2 forward 200" "cfg2 all 100" "cfg5 forward 200" "cfg4 forward 10" "cfg2 train 100" "cfg4 train 5"; do
   set -- $spec
-  run rocprof_$1_$2 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_$1_$2 -o run --output-format csv -- python tools/prof_target.py --workload $1 --mode $2 --launches 30
+  run rocprof_$1_$2 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_$1_$2 -o run --output-format csv -- python tools/prof_target.py --workload $1 --mode $2 --launches $3
+  python tools/trace_stats.py gpurun_out/prof_${TAG}_$1_$2/run_kernel_trace.csv $3 gpurun_out/prof_${TAG}_$1_$2/settled_stats.csv
 done
+run sweep_loss 300 python tools/batch_sweep.py loss
+run sweep_fwd 300 python tools/batch_sweep.py forward
 # PMC passes: HBM traffic (separate FETCH / WRITE passes) and issue counters
 VALU="SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM GRBM_GUI_ACTIVE"
 MFMA="SQ_WAVES SQ_INSTS_VALU_MFMA_F32 SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE"
@@ -37,7 +44,7 @@ for spec in "cfg2 loss k_sgpr" "cfg2 all k_valu" "cfg2 train k_vjp2" "cfg4 forwa
   rm -rf gpurun_out/pmc_${TAG}_$1_$2_$1
   CTR="$VALU"; case "$3" in k_wide*|k_vjp2|k_wdw*) CTR="$MFMA";; esac
   NL=20; [ "$1 $2" = "cfg4 train" ] && NL=2
-  run pmc_$1_$2 600 bash tools/gpu_pmc.sh ${TAG}_$1_$2 $1 "--mode $2 --launches $NL" "FETCH_SIZE" "WRITE_SIZE" "$CTR"
+  run pmc_$1_$2 600 bash tools/gpu_pmc.sh ${TAG}_$1_$2 $1 "--mode $2 --launches $NL --settle-s 0" "FETCH_SIZE" "WRITE_SIZE" "$CTR"
   python tools/pmc_summary.py gpurun_out/pmc_${TAG}_$1_$2_$1 $3 > gpurun_out/${TAG}_pmc_$1_$2.txt 2>&1
 done
 # the fused wide training sweeps, from the cfg4 train pass
