@@ -29,10 +29,10 @@ run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run 
 python tools/trace_stats.py gpurun_out/prof_$TAG/run_kernel_trace.csv 300 gpurun_out/prof_$TAG/settled_stats.csv
 # one kernel-trace summary per profiled pass, the clock settled first (0.3 s,
 # as bench.py), statistics over the last N calls only (tools/trace_stats.py)
-for spec in "cfg2 loss 200" "cfg2 forward 200" "cfg2 all 100" "cfg5 forward 200" "cfg4 forward 10" "cfg2 train 100" "cfg4 train 5"; do
+for spec in "cfg2 loss 200 k_sgpr" "cfg2 forward 200 k_sgpr" "cfg2 all 100 k_valu" "cfg5 forward 200 k_sgpr" "cfg4 forward 10 k_wide16" "cfg2 train 100 k_vjp2" "cfg4 train 5 k_wtrain16_fwd"; do
   set -- $spec
   run rocprof_$1_$2 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_$1_$2 -o run --output-format csv -- python tools/prof_target.py --workload $1 --mode $2 --launches $3
-  python tools/trace_stats.py gpurun_out/prof_${TAG}_$1_$2/run_kernel_trace.csv $3 gpurun_out/prof_${TAG}_$1_$2/settled_stats.csv
+  python tools/trace_stats.py gpurun_out/prof_${TAG}_$1_$2/run_kernel_trace.csv $3 gpurun_out/prof_${TAG}_$1_$2/settled_stats.csv $4
 done
 run sweep_loss 300 python tools/batch_sweep.py loss
 run sweep_fwd 300 python tools/batch_sweep.py forward

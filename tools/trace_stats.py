@@ -3,7 +3,7 @@ dispatches only: tools/prof_target.py settles the clock for --settle-s first
 (as bench.py does), and those settle launches must not enter the averages
 (round 5's traces were taken cold, so a kernel's average could exceed the
 bench's whole step).  usage:
-  trace_stats.py <kernel_trace.csv> <last_n_calls> [out.csv]
+  trace_stats.py <kernel_trace.csv> <last_n_calls> [out.csv|-] [first kernel of a call]
 For each kernel name: the number of its dispatches among the last
 last_n_calls * (dispatches per call) of the trace, their mean / median /
 min / max duration (ns), and the mean start-to-start spacing of the kernel
@@ -15,18 +15,26 @@ import sys
 
 def main():
     path, last = sys.argv[1], int(sys.argv[2])
-    out = sys.argv[3] if len(sys.argv) > 3 else None
+    out = sys.argv[3] if len(sys.argv) > 3 and sys.argv[3] != "-" else None
+    # optional: a substring of the name of the kernel that starts each call
+    # (a cfg4 training step is 39 dispatches whose tail repeats itself)
+    first_kernel = sys.argv[4] if len(sys.argv) > 4 else None
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     names = [r["Kernel_Name"] for r in rows]
     # dispatches per call: the trailing period of the kernel-name sequence
     per = 1
-    for p in range(1, 9):
-        tail = names[-4 * p:]
-        if len(tail) == 4 * p and all(tail[i] == tail[i % p] for i in range(len(tail))):
+    for p in range(1, 65):
+        reps = 4 if p <= 8 else 2  # a cfg4 training step is 39 dispatches
+        tail = names[-reps * p:]
+        if len(tail) == reps * p and all(tail[i] == tail[i % p] for i in range(len(tail))):
             per = p
             break
     sel = rows[-last * per:]
+    if first_kernel:
+        starts = [i for i, r in enumerate(rows) if first_kernel in r["Kernel_Name"]]
+        sel = rows[starts[-last]:]
+        per = round(len(sel) / last)
     by = {}
     for r in sel:
         by.setdefault(r["Kernel_Name"], []).append(
