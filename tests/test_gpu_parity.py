@@ -238,7 +238,9 @@ def test_nonaligned_input_view():
 def test_fused_forward_loss_matches_oracle(kind):
     flow = _make_flow(10, 6, [5, 5], 0.1, 9)
     stack = flow._native_stack()
-    for B in (1, 1000, 1 << 20, (1 << 23) + 77):
+    # 2^20 and 1310720 rows: 8 / 10 tiles per SIMD, which the grid runs on 4 / 5
+    # waves per SIMD instead of 6 (cnf_sgpr.hip grid_for); 2^23 + 77 on all 6
+    for B in (1, 1000, 1 << 20, 1310720, (1 << 23) + 77):
         x = _logits(B, 10, 11)
         y = torch.randint(0, 10, (B,), device=DEV, generator=torch.Generator(device=DEV).manual_seed(5))
         terms, z, ld = stack.forward_loss(x, y, kind=kind, det=0.5, want_outputs=True)
