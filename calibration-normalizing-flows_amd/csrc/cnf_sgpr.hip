@@ -543,7 +543,8 @@ __global__ __launch_bounds__(kWaves * 64, (waves_per_simd<MODE, ALL, PERM>())) v
   int t = gw;
   if (t < nfull) wave_dma<D, TR>(sm, in + (int64_t)t * TF, lane);
   // the wave with more tiles left goes first (VALU issue is arbitrated by
-  // priority, then age): the tail of a 2^20-row grid is 8 tiles on 6 waves
+  // priority, then age): waves of one SIMD may own unequal tile counts (2^23
+  // rows: 64 tiles on 6 waves; grid_for removes that only for short batches)
   auto set_prio = [&]() {
     --left;  // tiles after this one
     if (left >= 3) __builtin_amdgcn_s_setprio(3);
